@@ -1,0 +1,86 @@
+"""ctypes binding of libccmi.so (the C ABI declared in include/ccmi.h).
+
+The library is built in-tree (``make -C consensus_clustering_amd/csrc``, or
+``__graft_entry__.build()``) and loaded from this package directory.  There is
+no fallback: if the library is missing or fails to load, every GPU entry point
+raises, so a run can never silently measure or validate a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CCMI_LIB", os.path.join(_HERE, "libccmi.so"))
+
+_c_int, _c_i64, _c_u32, _c_sz, _c_dbl = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,
+                                         ctypes.c_size_t, ctypes.c_double)
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/ccmi.h
+SIGNATURES = {
+    "cc_version": (ctypes.c_char_p, []),
+    "cc_last_error": (ctypes.c_char_p, []),
+    "cc_resample_indices": (_c_int, [_c_u32, _c_int, _c_int, _c_int, _c_int, _vp, _c_int]),
+    "cc_random_sample": (_c_int, [_c_u32, _c_i64, _vp]),
+    "cc_num_tiles": (_c_i64, [_c_int]),
+    "cc_scatter_labels": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
+    "cc_cosample": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "cc_coassoc": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp,
+                            _vp, _vp]),
+    "cc_consensus": (_c_int, [_vp, _vp, _c_int, _vp, _vp]),
+    "cc_kmeans_workspace_bytes": (_c_sz, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int,
+                                          _c_int, _c_int]),
+    "cc_kmeans_batched": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int,
+                                   _c_int, _vp, _c_int, _c_int, _c_int, _c_dbl, _vp, _c_int, _vp,
+                                   _vp, _c_int, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class CCMIError(RuntimeError):
+    """A libccmi entry point returned a non-zero status."""
+
+
+def load():
+    """Load libccmi.so once; raise loudly if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise CCMIError(
+                f"libccmi.so not found at {LIB_PATH}: build it with "
+                "`make -C consensus_clustering_amd/csrc` (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(rc: int, fn: str):
+    if rc != 0:
+        msg = load().cc_last_error().decode(errors="replace")
+        raise CCMIError(f"{fn} failed ({rc}): {msg}")
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    check(rc, name)
+    return rc
+
+
+def ptr(t) -> int:
+    """Raw device/host pointer of a torch tensor or numpy array (None -> NULL)."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return t.data_ptr()
+    return t.ctypes.data

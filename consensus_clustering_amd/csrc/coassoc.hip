@@ -1,0 +1,435 @@
+// Co-sampling (I), co-association (M) and the fused consensus histogram on gfx950.
+//
+// Reference behaviour (consensus_clustering_parallelised.py, "CC.py"):
+//   I = S^T S over the H x n sampled-indicator matrix            CC.py:259-264
+//   M += L^T L over the K x n one-hot label matrix, per resample  CC.py:284-290
+//   C = f32(M) / f32(I + 1e-6); histogram of triu(C, 1), 20 bins  CC.py:338-344, :372
+//
+// Formulation.  With the labels of every resample stored sample-major as bytes
+// (labels_nh[i][h], 0xFF = not sampled), M_ij = sum over the virtual index
+// v = (h, c) of onehot_i(v) * onehot_j(v) with onehot_i(h, c) = [label_h(i) == c],
+// and I_ij the same sum over v = h with the sampled flag.  Both are int8 GEMMs
+// A * A^T with a 0/1 operand, run on v_mfma_i32_32x32x32_i8 with int32 accumulators:
+// exact integer counts.  The one-hot operand is never stored in HBM: each
+// super-step, every thread of the 512-thread workgroup loads the label bytes of ONE
+// row of the tile (A side or B side) for 128 virtual-k values, expands them to
+// 128 one-hot bytes in registers and writes them to LDS already in MFMA fragment
+// order (one ds_write_b128 per 16 bytes); the 8 waves then read fragments with
+// ds_read_b128 and issue 32 MFMAs each.  Channels are padded to KP = next pow2 >= K
+// so one virtual chunk of 32 holds 32/KP resamples (KP <= 32) or a channel slice.
+//
+// Tiling.  The n x n count matrix is covered by 256 x 256 tiles of the upper
+// triangle (bi <= bj), numbered row-major; a launch handles tiles
+// [tile_begin, tile_end), which is also how the triangle is row-band sharded over
+// GPUs.  Waves are arranged 2 x 4, each owning 128 x 64 outputs (4 x 2 blocks of
+// 32 x 32, 128 accumulator registers).
+//
+// Epilogue.  The I kernel stores its tile in accumulator order (uint16, coalesced)
+// so the M kernel re-reads exactly the I value of each of its own accumulator
+// elements.  The M kernel bins every strict-upper pair with numpy.histogram's
+// uniform-bin arithmetic (numpy/lib/_histograms_impl.py:851-868): x = f32(m) /
+// f32(f64(i) + 1e-6) correctly rounded, b = floor(f64(x) * 20), b == 20 -> 19,
+// then the two edge corrections against the float32 edges.  Per-thread private
+// LDS counters (ds_add, conflict-free [bin][thread] layout) are reduced per
+// workgroup and added to 20 uint64 global counters (integer atomics: order-free).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cmath>
+#include <string>
+
+#include "ccmi_internal.h"
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int T = CC_TILE;            // 256
+constexpr int NT = 512;               // threads per workgroup (8 waves)
+constexpr int KC = 4;                 // 32-wide k-chunks per super-step (128 virtual k)
+constexpr int FRAG = 1024;            // one 32x32x32 i8 operand fragment: 64 lanes x 16 B
+constexpr int SIDE = 8 * KC * FRAG;   // 8 row blocks x 4 chunks = 32 KiB
+constexpr int BUF = 2 * SIDE;         // A side + B side
+constexpr int LDS_BYTES = 2 * BUF;    // double buffered = 128 KiB
+constexpr int NBINS = CC_NBINS;
+
+__device__ __forceinline__ void tile_coords(int64_t t, int nb, int& bi, int& bj) {
+  auto start = [nb](int64_t b) -> int64_t { return b * nb - b * (b - 1) / 2; };
+  double a = 2.0 * nb + 1.0;
+  int r = static_cast<int>(floor((a - sqrt(a * a - 8.0 * static_cast<double>(t))) * 0.5));
+  r = r < 0 ? 0 : (r > nb - 1 ? nb - 1 : r);
+  while (r > 0 && start(r) > t) --r;
+  while (r + 1 < nb && start(r + 1) <= t) ++r;
+  bi = r;
+  bj = static_cast<int>(r + (t - start(r)));
+}
+
+// Histogram bin of one pair, exactly as numpy.histogram(bins=20, range=(0, 1)) on the
+// float32 consensus value (CC.py:339-344 -> _histograms_impl.py:851-868).
+__device__ __forceinline__ int consensus_bin(uint32_t m, uint32_t i, const float* e) {
+  const float fi = static_cast<float>(static_cast<double>(i) + 1e-6);
+  const float x = static_cast<float>(m) / fi;  // IEEE RN (no fast-math in this build)
+  int b = static_cast<int>(static_cast<double>(x) * 20.0);
+  if (b >= NBINS) b = NBINS - 1;
+  if (x < e[b]) b -= 1;
+  if (b != NBINS - 1 && x >= e[b + 1]) b += 1;
+  return b;
+}
+
+// Load the HS = 128/KP label bytes of one row for one super-step into w[].
+// Branch-free: an out-of-range row reads row 0 and is masked to 0xFF (= not sampled).
+template <int KP>
+__device__ __forceinline__ void load_labels(const uint8_t* rowp, bool valid, uint32_t (&w)[32]) {
+  constexpr int HS = 128 / KP;
+  const uint32_t msk = valid ? 0u : 0xFFFFFFFFu;
+  if constexpr (HS >= 16) {
+#pragma unroll
+    for (int q = 0; q < HS / 16; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(rowp)[q];
+      w[4 * q + 0] = v.x | msk;
+      w[4 * q + 1] = v.y | msk;
+      w[4 * q + 2] = v.z | msk;
+      w[4 * q + 3] = v.w | msk;
+    }
+  } else if constexpr (HS == 8) {
+    const uint2 v = *reinterpret_cast<const uint2*>(rowp);
+    w[0] = v.x | msk;
+    w[1] = v.y | msk;
+  } else if constexpr (HS == 4) {
+    w[0] = *reinterpret_cast<const uint32_t*>(rowp) | msk;
+  } else if constexpr (HS == 2) {
+    w[0] = 0xFFFF0000u | *reinterpret_cast<const uint16_t*>(rowp) | msk;
+  } else {
+    w[0] = 0xFFFFFF00u | *rowp | msk;
+  }
+}
+
+__device__ __forceinline__ uint32_t spread01(uint32_t v) {  // bits {0, 8} -> bits {0, 16}
+  return (v | (v << 8)) & 0x00010001u;
+}
+
+// Expand label bytes into 128 one-hot bytes (32 dwords): dword q holds virtual
+// k = 4q .. 4q+3 with k = h_local * KP + c (KP = 1: k = h_local, sampled flag).
+template <int KP>
+__device__ __forceinline__ void expand(const uint32_t (&w)[32], uint32_t (&o)[32]) {
+  if constexpr (KP == 1) {
+#pragma unroll
+    for (int q = 0; q < 32; ++q) o[q] = (~w[q] >> 7) & 0x01010101u;  // byte != 0xFF
+  } else if constexpr (KP == 2) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const uint32_t x = w[p];
+      const uint32_t is0 = ~x & 0x01010101u;               // label == 0
+      const uint32_t is1 = x & ~(x >> 1) & 0x01010101u;    // label == 1 (0xFF excluded)
+      o[2 * p + 0] = spread01(is0 & 0x101u) | (spread01(is1 & 0x101u) << 8);
+      o[2 * p + 1] = spread01((is0 >> 16) & 0x101u) | (spread01((is1 >> 16) & 0x101u) << 8);
+    }
+  } else {
+    constexpr int LOG = (KP == 4) ? 2 : (KP == 8) ? 3 : (KP == 16) ? 4 : (KP == 32) ? 5
+                      : (KP == 64) ? 6 : 7;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int k0 = 4 * q;
+      const int h = k0 >> LOG;
+      const uint32_t cq = static_cast<uint32_t>((k0 & (KP - 1)) >> 2);
+      const uint32_t lab = (w[h >> 2] >> (8 * (h & 3))) & 0xFFu;
+      o[q] = ((lab >> 2) == cq) ? (1u << ((lab & 3u) << 3)) : 0u;
+    }
+  }
+}
+
+template <int KP>
+__global__ __launch_bounds__(NT, 1) void tiles_kernel(
+    const uint8_t* __restrict__ labels, int n, int ldl, int Hpad, int64_t tile_begin,
+    uint16_t* __restrict__ I_tiles_out, const uint16_t* __restrict__ I_tiles_in,
+    const float* __restrict__ edges, unsigned long long* __restrict__ bin_counts,
+    int32_t* __restrict__ full_out) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  constexpr int HS = 128 / KP;  // resamples per super-step
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 2;  // 0..1 : 128-row half
+  const int wc = wave & 3;   // 0..3 : 64-col quarter
+  const int nb = (n + T - 1) / T;
+  const int64_t t = tile_begin + blockIdx.x;
+  int bi, bj;
+  tile_coords(t, nb, bi, bj);
+
+  // Expansion role: one row per thread. side 0 = tile rows (A), side 1 = tile cols (B).
+  const int side = tid >> 8;
+  const int erow = tid & 255;
+  const int grow = (side ? bj : bi) * T + erow;
+  const bool evalid = grow < n;
+  const uint8_t* rowp = labels + static_cast<int64_t>(evalid ? grow : 0) * ldl;
+  const int erb = erow >> 5, er = erow & 31;
+  char* const wbase = lds + side * SIDE + erb * KC * FRAG + er * 16;
+
+  const int nsteps = Hpad / HS;
+  v16i acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = v16i{};
+
+  uint32_t w[32], o[32];
+  load_labels<KP>(rowp, evalid, w);
+  expand<KP>(w, o);
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+      *reinterpret_cast<uint4*>(wbase + kc * FRAG + g * 512) =
+          make_uint4(o[kc * 8 + g * 4 + 0], o[kc * 8 + g * 4 + 1], o[kc * 8 + g * 4 + 2],
+                     o[kc * 8 + g * 4 + 3]);
+  __syncthreads();
+
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = (s + 1) < nsteps;
+    if (more) load_labels<KP>(rowp + (s + 1) * HS, evalid, w);
+    const char* rb = lds + (s & 1) * BUF;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      v4i a[4], b[2];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+        a[mi] = *reinterpret_cast<const v4i*>(rb + ((wr * 4 + mi) * KC + kc) * FRAG + lane * 16);
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+        b[nj] = *reinterpret_cast<const v4i*>(rb + SIDE + ((wc * 2 + nj) * KC + kc) * FRAG +
+                                              lane * 16);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj)
+          acc[mi][nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[nj], acc[mi][nj], 0, 0, 0);
+    }
+    if (more) {
+      expand<KP>(w, o);
+      char* wb = wbase + ((s + 1) & 1) * BUF;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+          *reinterpret_cast<uint4*>(wb + kc * FRAG + g * 512) =
+              make_uint4(o[kc * 8 + g * 4 + 0], o[kc * 8 + g * 4 + 1], o[kc * 8 + g * 4 + 2],
+                         o[kc * 8 + g * 4 + 3]);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue ------------------------------------------------------------
+  const int64_t tl = t - tile_begin;
+  const bool diag = (bi == bj);
+  const int row0 = bi * T + wr * 128 + 4 * (lane >> 5);
+  const int col0 = bj * T + wc * 64 + (lane & 31);
+
+  if constexpr (KP == 1) {
+    uint16_t* it = I_tiles_out + tl * (T * T);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int e = ((wave * 8 + mi * 2 + nj) * 16 + v) * 64 + lane;
+          const int val = acc[mi][nj][v];
+          it[e] = static_cast<uint16_t>(val);
+          if (full_out) {
+            const int i = row0 + mi * 32 + (v & 3) + 8 * (v >> 2);
+            const int j = col0 + nj * 32;
+            if (i < n && j < n) {
+              full_out[static_cast<int64_t>(i) * n + j] = val;
+              if (!diag) full_out[static_cast<int64_t>(j) * n + i] = val;
+            }
+          }
+        }
+  } else {
+    // [NBINS][NT] private counters + the 21 edges, reusing the operand LDS.
+    uint32_t* hist = reinterpret_cast<uint32_t*>(lds);
+    float* es = reinterpret_cast<float*>(lds + NBINS * NT * sizeof(uint32_t));
+#pragma unroll
+    for (int b = 0; b < NBINS; ++b) hist[b * NT + tid] = 0;
+    if (tid <= NBINS) es[tid] = edges[tid];
+    __syncthreads();
+    const uint16_t* it = I_tiles_in + tl * (T * T);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int e = ((wave * 8 + mi * 2 + nj) * 16 + v) * 64 + lane;
+          const uint32_t ival = it[e];
+          const int val = acc[mi][nj][v];
+          const int i = row0 + mi * 32 + (v & 3) + 8 * (v >> 2);
+          const int j = col0 + nj * 32;
+          if (i < j && j < n) {
+            const int b = consensus_bin(static_cast<uint32_t>(val), ival, es);
+            atomicAdd(&hist[b * NT + tid], 1u);
+          }
+          if (full_out && i < n && j < n) {
+            full_out[static_cast<int64_t>(i) * n + j] = val;
+            if (!diag) full_out[static_cast<int64_t>(j) * n + i] = val;
+          }
+        }
+    __syncthreads();
+    if (tid < NBINS) {
+      uint32_t sum = 0;
+      for (int k = 0; k < NT; ++k) sum += hist[tid * NT + k];
+      if (sum) atomicAdd(&bin_counts[tid], static_cast<unsigned long long>(sum));
+    }
+  }
+}
+
+__global__ void scatter_labels_kernel(const int32_t* __restrict__ idx, const int32_t* __restrict__ lab,
+                                      int H, int m, int n, uint8_t* __restrict__ out, int ldl) {
+  const int64_t total = static_cast<int64_t>(H) * m;
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int h = static_cast<int>(e / m);
+    const int row = idx[e];
+    if (row < 0 || row >= n) continue;
+    out[static_cast<int64_t>(row) * ldl + h] = lab ? static_cast<uint8_t>(lab[e]) : 0;
+  }
+}
+
+__global__ void consensus_kernel(const int32_t* __restrict__ M, const int32_t* __restrict__ I,
+                                 int n, float* __restrict__ C) {
+  const int64_t total = static_cast<int64_t>(n) * n;
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t i = e / n, j = e - i * n;
+    const float fi = static_cast<float>(static_cast<double>(I[e]) + 1e-6);
+    C[e] = (i == j) ? 1.0f : static_cast<float>(M[e]) / fi;
+  }
+}
+
+int check_common(const char* fn, const void* labels, int n, int ldl, int Hpad, int64_t tb,
+                 int64_t te) {
+  if (!labels || n <= 0 || Hpad <= 0 || Hpad % 128 != 0 || ldl < Hpad || ldl % 16 != 0) {
+    cc::set_error(std::string(fn) + ": bad labels/n/ldl/Hpad (Hpad % 128 == 0, ldl >= Hpad, ldl % 16 == 0)");
+    return CC_ERR_ARG;
+  }
+  if (Hpad > 65535) {
+    cc::set_error(std::string(fn) + ": Hpad > 65535 overflows the uint16 co-sampling tiles");
+    return CC_ERR_ARG;
+  }
+  const int64_t nt = cc_num_tiles(n);
+  if (tb < 0 || te < tb || te > nt) {
+    cc::set_error(std::string(fn) + ": tile range outside [0, num_tiles]");
+    return CC_ERR_ARG;
+  }
+  return CC_OK;
+}
+
+int launch_status(const char* fn) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cc::set_error(std::string(fn) + ": " + hipGetErrorString(e));
+    return CC_ERR_HIP;
+  }
+  return CC_OK;
+}
+
+template <int KP>
+void launch_tiles(dim3 grid, hipStream_t st, const uint8_t* lab, int n, int ldl, int Hpad,
+                  int64_t tb, uint16_t* Iout, const uint16_t* Iin, const float* edges,
+                  unsigned long long* counts, int32_t* full) {
+  hipLaunchKernelGGL(tiles_kernel<KP>, grid, dim3(NT), 0, st, lab, n, ldl, Hpad, tb, Iout, Iin,
+                     edges, counts, full);
+}
+
+}  // namespace
+
+extern "C" int64_t cc_num_tiles(int n) {
+  if (n <= 0) return 0;
+  const int64_t nb = (n + T - 1) / T;
+  return nb * (nb + 1) / 2;
+}
+
+extern "C" int cc_scatter_labels(const int32_t* idx_hm, const int32_t* labels_hm, int H, int m,
+                                 int n, int8_t* labels_nh, int ldl, void* stream) {
+  if (!idx_hm || !labels_nh || H < 0 || m < 0 || n <= 0 || ldl < H) {
+    cc::set_error("cc_scatter_labels: bad arguments (ldl >= H required)");
+    return CC_ERR_ARG;
+  }
+  const int64_t total = static_cast<int64_t>(H) * m;
+  if (total == 0) return CC_OK;
+  int blocks = static_cast<int>(std::min<int64_t>((total + 255) / 256, 8192));
+  hipLaunchKernelGGL(scatter_labels_kernel, dim3(blocks), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), idx_hm, labels_hm, H, m, n,
+                     reinterpret_cast<uint8_t*>(labels_nh), ldl);
+  return launch_status("cc_scatter_labels");
+}
+
+extern "C" int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, int64_t tile_begin,
+                           int64_t tile_end, uint16_t* I_tiles, int32_t* I_full, void* stream) {
+  int rc = check_common("cc_cosample", labels_nh, n, ldl, Hpad, tile_begin, tile_end);
+  if (rc) return rc;
+  if (!I_tiles) {
+    cc::set_error("cc_cosample: I_tiles is NULL");
+    return CC_ERR_ARG;
+  }
+  const int64_t ntl = tile_end - tile_begin;
+  if (ntl == 0) return CC_OK;
+  if (ntl > 0x7fffffff) {
+    cc::set_error("cc_cosample: too many tiles for one launch");
+    return CC_ERR_ARG;
+  }
+  launch_tiles<1>(dim3(static_cast<unsigned>(ntl)), static_cast<hipStream_t>(stream),
+                  reinterpret_cast<const uint8_t*>(labels_nh), n, ldl, Hpad, tile_begin, I_tiles,
+                  nullptr, nullptr, nullptr, I_full);
+  return launch_status("cc_cosample");
+}
+
+extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int K,
+                          int64_t tile_begin, int64_t tile_end, const uint16_t* I_tiles,
+                          const float* edges, unsigned long long* bin_counts, int32_t* M_full,
+                          void* stream) {
+  int rc = check_common("cc_coassoc", labels_nh, n, ldl, Hpad, tile_begin, tile_end);
+  if (rc) return rc;
+  if (K < 1 || K > 127) {
+    cc::set_error("cc_coassoc: K must be in [1, 127]");
+    return CC_ERR_ARG;
+  }
+  if (!I_tiles || !edges || !bin_counts) {
+    cc::set_error("cc_coassoc: I_tiles, edges and bin_counts are required");
+    return CC_ERR_ARG;
+  }
+  const int64_t ntl = tile_end - tile_begin;
+  if (ntl == 0) return CC_OK;
+  if (ntl > 0x7fffffff) {
+    cc::set_error("cc_coassoc: too many tiles for one launch");
+    return CC_ERR_ARG;
+  }
+  const dim3 grid(static_cast<unsigned>(ntl));
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint8_t* lab = reinterpret_cast<const uint8_t*>(labels_nh);
+  int kp = 2;
+  while (kp < K) kp <<= 1;
+  switch (kp) {
+    case 2: launch_tiles<2>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
+    case 4: launch_tiles<4>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
+    case 8: launch_tiles<8>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
+    case 16: launch_tiles<16>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
+    case 32: launch_tiles<32>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
+    case 64: launch_tiles<64>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
+    default: launch_tiles<128>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
+  }
+  return launch_status("cc_coassoc");
+}
+
+extern "C" int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stream) {
+  if (!M || !I || !C || n <= 0) {
+    cc::set_error("cc_consensus: bad arguments");
+    return CC_ERR_ARG;
+  }
+  const int64_t total = static_cast<int64_t>(n) * n;
+  int blocks = static_cast<int>(std::min<int64_t>((total + 255) / 256, 16384));
+  hipLaunchKernelGGL(consensus_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     M, I, n, C);
+  return launch_status("cc_consensus");
+}

@@ -1,0 +1,122 @@
+"""Device engine: torch-ROCm tensors as raw buffers around the libccmi C ABI.
+
+Torch is plumbing here (device memory, the current HIP stream, torch.distributed);
+every count, label and histogram is produced by the gfx950 kernels in
+``csrc/`` through ``_lib``.  No function in this module has a CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .post import N_BINS, bin_edges32
+
+TILE = 256
+HALIGN = 128  # resample padding of the sample-major label matrix (Hpad % 128 == 0)
+
+
+def require_gpu(device=None) -> torch.device:
+    """The torch device to run on; raises if there is no GPU or no libccmi.so."""
+    if not torch.cuda.is_available():
+        raise _lib.CCMIError(
+            "consensus_clustering_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+    _lib.load()
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(device)
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def pad_h(H: int) -> int:
+    return ((H + HALIGN - 1) // HALIGN) * HALIGN
+
+
+def num_tiles(n: int) -> int:
+    return int(_lib.load().cc_num_tiles(int(n)))
+
+
+# ---------------------------------------------------------------- host-native RNG
+
+def resample_indices(seed: int, n: int, m: int, h_begin: int, h_end: int, n_threads: int = 0) -> np.ndarray:
+    """int32 [h_end-h_begin, m]: RandomState(seed+h).choice(n, m, replace=False) (CC.py:231-239)."""
+    if seed is None:
+        # the reference computes `self.random_state + i` (CC.py:232)
+        raise TypeError("unsupported operand type(s) for +: 'NoneType' and 'int'")
+    seed = int(seed)
+    if seed < 0 or seed + h_end - 1 > 2**32 - 1:
+        raise ValueError("Seed must be between 0 and 2**32 - 1")
+    out = np.empty((h_end - h_begin, m), dtype=np.int32)
+    _lib.call("cc_resample_indices", ctypes.c_uint32(seed), h_begin, h_end, n, m,
+              out.ctypes.data, n_threads)
+    return out
+
+
+def random_sample(seed: int, count: int) -> np.ndarray:
+    """RandomState(seed).random_sample(count) via the native MT19937."""
+    out = np.empty(count, dtype=np.float64)
+    _lib.call("cc_random_sample", ctypes.c_uint32(int(seed)), int(count),
+              out.ctypes.data if count else None)
+    return out
+
+
+# ---------------------------------------------------------------- label matrices
+
+def new_label_matrix(nK: int, n: int, Hpad: int, device) -> torch.Tensor:
+    """uint8 [nK, n, Hpad] filled with 0xFF (= not sampled)."""
+    return torch.full((nK, n, Hpad), 0xFF, dtype=torch.uint8, device=device)
+
+
+def scatter_labels(idx_hm: torch.Tensor, labels_hm, n: int, out_nh: torch.Tensor, h_offset: int = 0):
+    """out_nh[idx[h, r], h_offset + h] = labels[h, r] (or 0 when labels_hm is None)."""
+    H, m = idx_hm.shape
+    assert idx_hm.dtype == torch.int32 and idx_hm.is_contiguous()
+    assert out_nh.dtype == torch.uint8 and out_nh.dim() == 2 and out_nh.shape[0] == n
+    assert out_nh.stride(1) == 1
+    ldl = out_nh.stride(0)
+    if labels_hm is not None:
+        assert labels_hm.dtype == torch.int32 and tuple(labels_hm.shape) == (H, m)
+        labels_hm = labels_hm.contiguous()
+    base = out_nh[:, h_offset:]
+    _lib.call("cc_scatter_labels", _lib.ptr(idx_hm), _lib.ptr(labels_hm), H, m, n,
+              base.data_ptr(), ldl, stream_ptr())
+
+
+# ---------------------------------------------------------------- co-sampling / co-association
+
+def cosample(labels_nh: torch.Tensor, n: int, Hpad: int, tile_begin: int, tile_end: int,
+             want_full: bool = False):
+    """I tiles (uint16 accumulator order) for [tile_begin, tile_end), optional full int32 I."""
+    dev = labels_nh.device
+    ntl = tile_end - tile_begin
+    I_tiles = torch.empty((max(ntl, 0), TILE * TILE), dtype=torch.int16, device=dev)
+    I_full = torch.zeros((n, n), dtype=torch.int32, device=dev) if want_full else None
+    _lib.call("cc_cosample", labels_nh.data_ptr(), n, labels_nh.stride(0), Hpad, tile_begin,
+              tile_end, I_tiles.data_ptr(), _lib.ptr(I_full), stream_ptr())
+    return I_tiles, I_full
+
+
+def edges_device(device) -> torch.Tensor:
+    return torch.from_numpy(bin_edges32().copy()).to(device)
+
+
+def coassoc(labels_nh: torch.Tensor, n: int, Hpad: int, K: int, tile_begin: int, tile_end: int,
+            I_tiles: torch.Tensor, edges: torch.Tensor, counts: torch.Tensor,
+            M_full: torch.Tensor = None):
+    """Accumulate the strict-upper-pair histogram of C for one K into counts (int64[20])."""
+    assert counts.dtype == torch.int64 and counts.numel() == N_BINS
+    _lib.call("cc_coassoc", labels_nh.data_ptr(), n, labels_nh.stride(0), Hpad, int(K),
+              tile_begin, tile_end, I_tiles.data_ptr(), edges.data_ptr(), counts.data_ptr(),
+              _lib.ptr(M_full), stream_ptr())
+
+
+def consensus(M: torch.Tensor, I: torch.Tensor) -> torch.Tensor:
+    n = M.shape[0]
+    C = torch.empty((n, n), dtype=torch.float32, device=M.device)
+    _lib.call("cc_consensus", M.data_ptr(), I.data_ptr(), n, C.data_ptr(), stream_ptr())
+    return C

@@ -1,0 +1,79 @@
+"""Host post-processing: 20 int64 bin counts -> the reference's per-K result fields.
+
+The device never materialises the consensus matrix on the hot path; it returns
+the exact numpy.histogram bin counts of ``triu(C, 1).ravel()`` (strict upper
+triangle only, see ``pair_counts_to_hist_counts``).  From those counts this
+module rebuilds ``hist``, ``cdf``, ``bin_edges`` and ``pac_area`` bit-for-bit as
+``_get_cdf_data`` computes them (reference ``consensus_clustering_parallelised.py``
+:316-354), under numpy-2 (NEP 50) semantics:
+
+* ``bin_edges`` are float32 (``np.linspace(0, 1, 21, dtype=float32)``, numpy
+  ``_histograms_impl.py:444-452``), so ``dbin`` is ``np.float32(0.05)``;
+* ``hist = counts / diff(edges).astype(float) / counts.sum()``
+  (``_histograms_impl.py:900-901``);
+* ``cdf = cumsum(hist) * dbin``; ``pac = cdf[int(u2/dbin) - 1] - cdf[int(u1/dbin)]``
+  with float32 scalar division (u1_ind=2, u2_ind=18 for the default interval).
+
+The north-star extensions ``cdf_area``, ``delta_k`` and ``best_k`` (no reference
+implementation) are defined here.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+N_BINS = 20
+
+
+def bin_edges32() -> np.ndarray:
+    """The exact float32 edges numpy.histogram uses for bins=20, range=(0, 1) on float32 data."""
+    return np.histogram(np.zeros(1, dtype=np.float32), bins=N_BINS, range=(0, 1))[1]
+
+
+def pair_counts_to_hist_counts(pair_counts, n: int) -> np.ndarray:
+    """Add the n(n+1)/2 zeros that ``np.triu(C, k=1).ravel()`` contributes to bin 0.
+
+    ``pair_counts`` are the bins of the n(n-1)/2 strict-upper-triangle pairs (CC.py:338).
+    """
+    c = np.asarray(pair_counts, dtype=np.int64).copy()
+    if c.shape != (N_BINS,):
+        raise ValueError(f"expected {N_BINS} bin counts, got shape {c.shape}")
+    c[0] += n * (n + 1) // 2
+    return c
+
+
+def cdf_from_counts(hist_counts, PAC_interval=(0.1, 0.9)):
+    """hist, cdf, bin_edges, pac_area from int64 histogram counts (CC.py:339-352)."""
+    n = np.asarray(hist_counts, dtype=np.intp)
+    bin_edges = bin_edges32()
+    db = np.array(np.diff(bin_edges), float)
+    hist = n / db / n.sum()
+    dbin = bin_edges[1] - bin_edges[0]
+    cdf = np.cumsum(hist) * dbin
+    u1, u2 = PAC_interval
+    u1_ind = int(u1 / dbin)
+    u2_ind = int(u2 / dbin)
+    pac_area = cdf[u2_ind - 1] - cdf[u1_ind]
+    return hist, cdf, bin_edges, pac_area
+
+
+def cdf_area(cdf, bin_edges) -> float:
+    """Monti area under the binned CDF: Σ_b (edges[b+1] - edges[b]) · cdf[b] in float64."""
+    widths = np.diff(np.asarray(bin_edges, dtype=np.float64))
+    return float(np.sum(widths * np.asarray(cdf, dtype=np.float64)))
+
+
+def delta_k(areas: dict) -> dict:
+    """Monti Δ(K): first K -> A(K); later K -> (A(K) - A(K_prev)) / A(K_prev), in K_range order."""
+    out, prev = {}, None
+    for K, A in areas.items():
+        out[K] = A if prev is None else (A - prev) / prev if prev != 0 else float("inf")
+        prev = A
+    return out
+
+
+def best_k(pac: dict):
+    """K with the smallest PAC area; ties -> first K in K_range order (np.argmin semantics)."""
+    Ks = list(pac.keys())
+    if not Ks:
+        return None
+    return Ks[int(np.argmin(np.array([pac[K] for K in Ks], dtype=np.float64)))]

@@ -1,0 +1,120 @@
+/*
+ * ccmi.h — C ABI of the MI355X-native consensus-clustering engine (libccmi.so).
+ *
+ * Plain C: pointers, sizes and a hipStream_t passed as void*.  No C++ or torch
+ * types cross this boundary.  Every entry point returns 0 on success and a
+ * negative code on error; the message is available from cc_last_error() on the
+ * calling thread.  Device pointers are caller-owned (the Python host passes
+ * torch-ROCm tensors' data_ptr()); the library allocates nothing on the device.
+ * Launches are asynchronous on the given stream and safe to capture in a graph.
+ *
+ * Each entry point replaces a piece of the reference's hot path
+ * (/root/reference/consensus_clustering_parallelised.py, "CC.py" below):
+ *
+ *   cc_resample_indices   CC.py:216-241  _get_subsampling_indices (numpy RandomState replay)
+ *   cc_kpp_first_pos      sklearn _kmeans.py:225 first k-means++ centre (RandomState.choice with p)
+ *   cc_scatter_labels     CC.py:260-262, :284-285  indicator / one-hot row placement
+ *   cc_cosample           CC.py:264  I = S^T S            (int8 MFMA, upper-triangle tiles)
+ *   cc_coassoc            CC.py:287-290 + :338-344  M += L^T L fused with the 20-bin histogram
+ *   cc_consensus          CC.py:372-373  C = f32(M) / f32(I + 1e-6), diag 1
+ *   cc_kmeans_batched     CC.py:282 clusterer.fit_predict for every (h, K) at once
+ *                         (sklearn KMeans: k-means++ init, Lloyd, best of n_init)
+ */
+#ifndef CCMI_H
+#define CCMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CC_OK 0
+#define CC_ERR_ARG (-1)
+#define CC_ERR_HIP (-2)
+#define CC_ERR_UNSUPPORTED (-3)
+
+/* Tile edge of the upper-triangle tiling used by cc_cosample / cc_coassoc. */
+#define CC_TILE 256
+/* Number of consensus-histogram bins (CC.py:316 bins=20). */
+#define CC_NBINS 20
+
+const char* cc_version(void);
+const char* cc_last_error(void);
+
+/* ---- host-side helpers (native, no device) ------------------------------ */
+
+/* Resample indices of CC.py:231-239 for h in [h_begin, h_end):
+ * out[(h-h_begin)*m + r] = numpy.random.RandomState(seed + h).permutation(n)[r], r < m
+ * (RandomState.choice(n, m, replace=False) == permutation(n)[:m]).  MT19937
+ * init_genrand + legacy random_interval rejection sampling, bit-identical to
+ * numpy 1.17+ legacy RandomState.  Runs on n_threads host threads (<=0: all). */
+int cc_resample_indices(uint32_t seed, int h_begin, int h_end, int n, int m, int32_t* out,
+                        int n_threads);
+
+/* Raw doubles of numpy.random.RandomState(seed).random_sample(count). */
+int cc_random_sample(uint32_t seed, int64_t count, double* out);
+
+/* Number of tiles of the CC_TILE upper-triangle tiling for n samples. */
+int64_t cc_num_tiles(int n);
+
+/* ---- device kernels ----------------------------------------------------- */
+
+/* labels_nh[idx[h][r] * ldl + h] = labels_hm ? labels_hm[h*m + r] : 0 for h < H, r < m.
+ * labels_nh must be pre-filled with 0xFF (= not sampled).  (CC.py:260-262, :284-285) */
+int cc_scatter_labels(const int32_t* idx_hm, const int32_t* labels_hm, int H, int m, int n,
+                      int8_t* labels_nh, int ldl, void* stream);
+
+/* Co-sampling counts I_ij = #{h : i and j both sampled} for the tiles
+ * [tile_begin, tile_end) of the upper-triangle tiling (CC.py:264).
+ * labels_nh: [n][ldl] int8, 0xFF = not sampled; Hpad (multiple of 128, <= ldl) columns used.
+ * I_tiles:   [tile_end - tile_begin][CC_TILE*CC_TILE] uint16, accumulator order (device-private).
+ * I_full:    optional [n][n] int32 (both triangles), may be NULL. */
+int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, int64_t tile_begin,
+                int64_t tile_end, uint16_t* I_tiles, int32_t* I_full, void* stream);
+
+/* Co-association counts M_ij = #{h : label_h(i) == label_h(j) >= 0} for the same
+ * tiles, fused with the numpy-exact 20-bin histogram of C = f32(M)/f32(I+1e-6)
+ * over the strict upper triangle i < j (CC.py:287-290, :338-344).
+ * edges: 21 float32 bin edges (numpy's), device.  bin_counts: [20] uint64, device,
+ * accumulated into (not cleared).  M_full: optional [n][n] int32, may be NULL.
+ * K <= 127. */
+int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int K, int64_t tile_begin,
+               int64_t tile_end, const uint16_t* I_tiles, const float* edges,
+               unsigned long long* bin_counts, int32_t* M_full, void* stream);
+
+/* C = f32(M) / f32(f64(I) + 1e-6) with C_ii = 1 (CC.py:372-373), [n][n]. */
+int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stream);
+
+/* Batched k-means for every (resample h, K, init) problem (sklearn KMeans
+ * semantics: k-means++ with 2+floor(ln K) local trials, Lloyd with strict/tol
+ * convergence and empty-cluster relocation, best of n_init).
+ *
+ *  X        [n][ldx] float32, mean-centred, zero-padded to dpad columns (device)
+ *  xnorm    [n] float32 squared row norms of X (device)
+ *  idx_hm   [H][m] int32 resample rows (device); problems use h in [h_begin, h_end)
+ *  Ks       [nK] K values (host)
+ *  kpp_u    [nK][n_init][1 + (Kmax-1)*ntrials_max] doubles: per-(K,init) uniforms of
+ *           RandomState(seed) (entry 0 unused; first centre given by kpp_pos) (device)
+ *  kpp_pos  [nK][n_init] int32 first-centre row positions (device)
+ *  labels_nh  [nK][n][ldl] int8 output, pre-filled 0xFF (device)
+ *  inertia  optional [nK][H] float32 best inertia (device) ; n_iter optional [nK][H] int32
+ *  stats    optional [4] uint64 (device, accumulated): {lloyd row-centroid dots,
+ *           seeding row-candidate dots, sweeps, relocations}
+ *  workspace / ws_bytes: from cc_kmeans_workspace_bytes with the same arguments. */
+size_t cc_kmeans_workspace_bytes(int n, int dpad, int H, int m, const int32_t* Ks, int nK,
+                                 int n_init, int h_begin, int h_end);
+int cc_kmeans_batched(const float* X, const float* xnorm, int n, int dpad, int ldx,
+                      const int32_t* idx_hm, int H, int m, int h_begin, int h_end,
+                      const int32_t* Ks, int nK, int n_init, int max_iter, double tol_rel,
+                      const double* kpp_u, int kpp_stride, const int32_t* kpp_pos,
+                      int8_t* labels_nh, int ldl, float* inertia, int32_t* n_iter,
+                      unsigned long long* stats, void* workspace, size_t ws_bytes,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CCMI_H */

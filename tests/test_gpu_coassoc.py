@@ -1,0 +1,126 @@
+"""Label-injection parity (SURVEY §4 layer 2): the reference's own labels go into the gfx950
+co-sampling / co-association / histogram kernels, which must reproduce the reference's
+mij, iij and histogram counts bit-for-bit (and hence hist/cdf/pac after host post-processing)."""
+import numpy as np
+import pytest
+import torch
+
+from consensus_clustering_amd import engine, post
+from oracle import cc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_labels(idx, labels_list, n, H, dev):
+    Hpad = engine.pad_h(H)
+    idx_d = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int32)).to(dev)
+    L = engine.new_label_matrix(len(labels_list), n, Hpad, dev)
+    for j, lab in enumerate(labels_list):
+        lab_d = torch.from_numpy(np.ascontiguousarray(lab, dtype=np.int32)).to(dev)
+        engine.scatter_labels(idx_d, lab_d, n, L[j])
+    return L, Hpad
+
+
+def _run(L, n, Hpad, Ks, tile_ranges=None, want_full=True):
+    dev = L.device
+    nt = engine.num_tiles(n)
+    tile_ranges = tile_ranges or [(0, nt)]
+    edges = engine.edges_device(dev)
+    I_full = torch.zeros((n, n), dtype=torch.int32, device=dev) if want_full else None
+    counts = torch.zeros((len(Ks), 20), dtype=torch.int64, device=dev)
+    Ms = [torch.zeros((n, n), dtype=torch.int32, device=dev) if want_full else None for _ in Ks]
+    for (tb, te) in tile_ranges:
+        I_tiles, I_part = engine.cosample(L[0], n, Hpad, tb, te, want_full=want_full)
+        if want_full:
+            I_full += I_part
+        for j, K in enumerate(Ks):
+            Mp = torch.zeros((n, n), dtype=torch.int32, device=dev) if want_full else None
+            engine.coassoc(L[j], n, Hpad, int(K), tb, te, I_tiles, edges, counts[j], Mp)
+            if want_full:
+                Ms[j] += Mp
+    torch.cuda.synchronize()
+    return (I_full.cpu().numpy() if want_full else None,
+            [M.cpu().numpy() if want_full else None for M in Ms], counts.cpu().numpy())
+
+
+def test_fixture_label_injection(fixture):
+    dev = engine.require_gpu()
+    n = fixture["X"].shape[0]
+    H = fixture["meta"]["H"]
+    Ks = [int(k) for k in fixture["K_range"]]
+    L, Hpad = _device_labels(fixture["indices"], list(fixture["labels"]), n, H, dev)
+    I, Ms, counts = _run(L, n, Hpad, Ks)
+    dt = O.reference_dtype(H)
+    np.testing.assert_array_equal(I.astype(dt), fixture["iij"])
+    for j, K in enumerate(Ks):
+        np.testing.assert_array_equal(Ms[j].astype(dt), fixture["mij"][j])
+        hist, cdf, edges, pac = post.cdf_from_counts(post.pair_counts_to_hist_counts(counts[j], n))
+        np.testing.assert_array_equal(hist, fixture["hist"][j])
+        np.testing.assert_array_equal(cdf, fixture["cdf"][j])
+        np.testing.assert_array_equal(edges, fixture["bin_edges"][j])
+        assert pac == fixture["pac_area"][j]
+
+
+def _random_case(n, H, frac, Ks, seed):
+    rng = np.random.default_rng(seed)
+    m = int(frac * n)
+    idx = np.stack([rng.permutation(n)[:m] for _ in range(H)]).astype(np.int32)
+    truth = rng.integers(0, 7, size=n)
+    labs = []
+    for K in Ks:
+        lab = np.empty((H, m), dtype=np.int32)
+        for h in range(H):
+            noisy = (truth[idx[h]] + (rng.random(m) < 0.15) * rng.integers(0, K, size=m)) % K
+            lab[h] = noisy
+        labs.append(lab)
+    return idx, labs
+
+
+@pytest.mark.parametrize("n,H,frac,Ks", [
+    (700, 200, 0.8, [2, 3, 5, 9, 17]),
+    (300, 131, 0.6, [33, 100, 127]),
+    (513, 300, 0.9, [4, 8, 16, 32]),
+])
+def test_random_labels_vs_oracle(n, H, frac, Ks):
+    dev = engine.require_gpu()
+    idx, labs = _random_case(n, H, frac, Ks, seed=n + H)
+    L, Hpad = _device_labels(idx, labs, n, H, dev)
+    I, Ms, counts = _run(L, n, Hpad, Ks)
+    I_ref = O.cosample_matrix(idx.astype(np.int64), n)
+    np.testing.assert_array_equal(I, I_ref)
+    iu = np.triu_indices(n, 1)
+    for j, K in enumerate(Ks):
+        M_ref = O.coassoc_matrix(idx.astype(np.int64), labs[j].astype(np.int64), K, n)
+        np.testing.assert_array_equal(Ms[j], M_ref)
+        C = O.consensus_matrix(M_ref.astype(np.uint16), I_ref.astype(np.uint16))
+        pair, _ = np.histogram(C[iu], bins=20, range=(0, 1))
+        np.testing.assert_array_equal(counts[j], pair)
+
+
+def test_tile_range_sharding_is_exact():
+    """Row-band sharding of the triangle (multi-GPU mode B) sums to the single-range result."""
+    dev = engine.require_gpu()
+    n, H, Ks = 900, 150, [3, 6]
+    idx, labs = _random_case(n, H, 0.8, Ks, seed=3)
+    L, Hpad = _device_labels(idx, labs, n, H, dev)
+    nt = engine.num_tiles(n)
+    I1, M1, c1 = _run(L, n, Hpad, Ks)
+    cuts = [(0, 2), (2, 5), (5, nt)]
+    I2, M2, c2 = _run(L, n, Hpad, Ks, tile_ranges=cuts)
+    np.testing.assert_array_equal(I1, I2)
+    np.testing.assert_array_equal(c1, c2)
+    for a, b in zip(M1, M2):
+        np.testing.assert_array_equal(a, b)
+    _, _, c3 = _run(L, n, Hpad, Ks, want_full=False)
+    np.testing.assert_array_equal(c1, c3)
+
+
+def test_consensus_matrix_kernel():
+    dev = engine.require_gpu()
+    rng = np.random.default_rng(0)
+    n = 333
+    I = rng.integers(0, 1001, size=(n, n)).astype(np.int32)
+    I = np.maximum(I, I.T)
+    M = (I * rng.random((n, n))).astype(np.int32)
+    C = engine.consensus(torch.from_numpy(M).to(dev), torch.from_numpy(I).to(dev)).cpu().numpy()
+    np.testing.assert_array_equal(C, O.consensus_matrix(M.astype(np.uint16), I.astype(np.uint16)))
