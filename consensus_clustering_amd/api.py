@@ -1,0 +1,279 @@
+"""Drop-in ``ConsensusClustering`` (reference: consensus_clustering_parallelised.py, "CC.py").
+
+Same constructor keywords (CC.py:21-36), ``fit(X) -> self`` (CC.py:92-136) and the same
+per-K result dict ``cdf_at_K_data[K]`` with keys consensus_labels, hist, cdf, bin_edges,
+pac_area, mij, iij, cij and the reference's dtypes (CC.py:378-387): mij/iij in uint8
+when n_iterations < 256 else uint16 (CC.py:107), cij float32 with a unit diagonal,
+bin_edges float32, hist/cdf float64, pac_area np.float64.
+
+What runs where (``fit``):
+  resampling      host-native numpy-RandomState replay (libccmi cc_resample_indices)
+  clustering      default clusterer (KMeans) -> all (h, K, init) problems in batched
+                  gfx950 launches (cc_kmeans_batched); any other plugin clusterer
+                  (e.g. GaussianMixture) keeps the reference's host fit_predict per
+                  (K, h) and only its labels go to the GPU (hybrid path)
+  I, M, histogram int8-MFMA tiles of the upper triangle (cc_cosample / cc_coassoc)
+  hist/cdf/PAC    host float64 from 20 exact integer counts (post.py)
+  multi-GPU       resamples and triangle tiles sharded over torch.distributed ranks
+                  (dist.py); RCCL MIN-merge of labels, SUM of counts
+
+Deliberate differences, all documented in DESIGN.md: the constructor does not delete
+files in ``memmap_folder`` (CC.py:83-86); the n x n matrices are materialised only when
+``keep_matrices`` (default: n <= 20000) since the reference's O(n^2)-per-K retention is
+infeasible at n = 50k; parallel arguments (n_jobs, parallelization_method) are accepted
+and ignored (the reference's threads/processes paths race).
+Additions: ``cdf_area_``, ``delta_k_``, ``pac_area_``, ``best_k_`` and ``predict``.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from . import dist, engine, post
+from .kmeans import BatchedKMeans
+
+
+def _default_kmeans():
+    from sklearn.cluster import KMeans
+
+    return KMeans()
+
+
+def _is_default_kmeans(est) -> bool:
+    """KMeans configured so that the batched gfx950 k-means reproduces it."""
+    try:
+        from sklearn.cluster import KMeans
+    except ImportError:  # pragma: no cover
+        return False
+    if type(est) is not KMeans:
+        return False
+    p = est.get_params()
+    return (isinstance(p.get("init"), str) and p["init"] == "k-means++"
+            and p.get("algorithm", "lloyd") in ("lloyd", "auto", "full")
+            and p.get("n_init") is not None)
+
+
+class ConsensusClustering:
+    """Monti consensus clustering on MI355X.  Drop-in for CC.py:11."""
+
+    def __init__(
+        self,
+        clusterer=None,
+        clusterer_options={'n_init': 3},
+        K_range=(2, 3),
+        n_iterations=25,
+        subsampling=0.8,
+        random_state=None,
+        consensus_matrix_analysis='PAC',
+        PAC_interval=(0.1, 0.9),
+        plot_cdf=True,
+        agg_clustering_linkage='average',
+        n_jobs=1,
+        parallelization_method='multithreading',
+        memmap_folder='./memmap',
+        *,
+        keep_matrices='auto',
+        device=None,
+        workspace_budget=8 << 30,
+    ):
+        self.K_range = K_range
+        self.n_iterations = n_iterations
+        self.subsampling = subsampling
+        self.clusterer = clusterer
+        self.clusterer_options = clusterer_options
+
+        self.consensus_matrix_analysis = consensus_matrix_analysis
+        self.PAC_interval = PAC_interval
+        self.plot_cdf = plot_cdf
+        self.agg_clustering_linkage = agg_clustering_linkage
+
+        self.random_state = random_state
+        self.n_jobs = n_jobs
+        self.parallelization_method = parallelization_method
+        self.memmap_folder = memmap_folder  # kept for compatibility; never touched
+
+        self.keep_matrices = keep_matrices
+        self.device = device
+        self.workspace_budget = workspace_budget
+        self.timings_ = {}
+
+        if self.clusterer is None:
+            print('KMeans is set as default clusterer')
+            self.clusterer = _default_kmeans()
+
+    # ------------------------------------------------------------------ plugin
+    def _set_clusterer_K(self):
+        """CC.py:201-214: set n_clusters / n_components, then set_params(random_state, **opts)."""
+        if hasattr(self.clusterer, 'n_clusters'):
+            self.clusterer.n_clusters = self._K
+        elif hasattr(self.clusterer, 'n_components'):
+            self.clusterer.n_components = self._K
+        else:
+            raise AttributeError('clusterer has neither n_clusters nor n_components attribute')
+        self.clusterer.set_params(random_state=self.random_state, **self.clusterer_options)
+
+    def _kmeans_params(self):
+        """The KMeans parameters after the reference's set_params (clusterer_options win)."""
+        Ks = list(self.K_range)
+        if not Ks:
+            return None
+        self._K = Ks[0]
+        self._set_clusterer_K()
+        if not _is_default_kmeans(self.clusterer):
+            return None
+        p = self.clusterer.get_params()
+        n_init = p["n_init"]
+        if n_init == "auto":
+            n_init = 1  # sklearn: 'auto' -> 1 run for init='k-means++'
+        return dict(n_init=int(n_init), max_iter=int(p["max_iter"]), tol=float(p["tol"]))
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, X):
+        """Fit on X [n_samples, n_features] and fill ``cdf_at_K_data`` (CC.py:92-136)."""
+        t_start = time.perf_counter()
+        X = np.asarray(X)
+        self._N, _ = X.shape
+        self._dtype = np.uint8 if self.n_iterations < 256 else np.uint16
+        self.cdf_at_K_data = dict()
+        n, H = self._N, int(self.n_iterations)
+        m = int(self.subsampling * n)
+        Ks = [int(K) for K in self.K_range]
+        rank, W = dist.world()
+        dev = engine.require_gpu(self.device)
+        keep = self.keep_matrices
+        if keep == 'auto':
+            keep = n <= 20000
+
+        # resampling (CC.py:216-241): every rank draws all H (needed by nobody else, cheap)
+        h0, h1 = dist.shard(H, rank, W)
+        idx = engine.resample_indices(self.random_state, n, m, 0, H)
+        idx_d = torch.from_numpy(idx).to(dev)
+        Hpad = engine.pad_h(H)
+        labels = engine.new_label_matrix(max(len(Ks), 1), n, Hpad, dev)
+        t_rs = time.perf_counter()
+
+        km = self._kmeans_params()
+        self.backend_ = 'gpu-kmeans' if km is not None else 'host-clusterer'
+        if Ks and km is not None:
+            Xd, xnorm, _ = _prepare(X, dev)
+            bk = BatchedKMeans(Ks, n_init=km["n_init"], max_iter=km["max_iter"], tol=km["tol"],
+                               random_state=self.random_state,
+                               workspace_budget=self.workspace_budget)
+            self.kmeans_inertia_ = torch.zeros((len(Ks), H), dtype=torch.float32, device=dev)
+            self.kmeans_n_iter_ = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
+            bk.run(Xd, xnorm, X.shape[1], idx_d, n, H, m, h0, h1, labels,
+                   weight_dtype=X.dtype if X.dtype in (np.float32, np.float64) else np.float64,
+                   inertia=self.kmeans_inertia_, n_iter=self.kmeans_n_iter_)
+            self.kmeans_stats_ = bk.stats
+        elif Ks:
+            for k, K in enumerate(Ks):
+                self._K = K
+                self._set_clusterer_K()
+                lab = np.empty((h1 - h0, m), dtype=np.int32)
+                for h in range(h0, h1):
+                    lab[h - h0] = np.asarray(self.clusterer.fit_predict(X[idx[h]]))
+                if lab.size and (lab.min() < 0 or lab.max() >= min(K, 128)):
+                    raise ValueError(f"clusterer labels must lie in [0, {K}) and K <= 127")
+                engine.scatter_labels(idx_d[h0:h1].contiguous(), torch.from_numpy(lab).to(dev), n,
+                                      labels[k], h_offset=h0)
+        dist.merge_labels(labels)
+        torch.cuda.synchronize(dev)
+        t_cl = time.perf_counter()
+
+        # co-sampling, co-association and histogram over this rank's band of tiles
+        nt = engine.num_tiles(n)
+        t0, t1 = dist.shard(nt, rank, W)
+        I_tiles, I_full = engine.cosample(labels[0], n, Hpad, t0, t1, want_full=keep)
+        edges = engine.edges_device(dev)
+        counts = torch.zeros((len(Ks), post.N_BINS), dtype=torch.int64, device=dev)
+        M_full = [None] * len(Ks)
+        for k, K in enumerate(Ks):
+            if keep:
+                M_full[k] = torch.zeros((n, n), dtype=torch.int32, device=dev)
+            engine.coassoc(labels[k], n, Hpad, K, t0, t1, I_tiles, edges, counts[k], M_full[k])
+        dist.sum_counts(counts)
+        if keep:
+            dist.sum_counts(I_full)
+            for M in M_full:
+                dist.sum_counts(M)
+        counts_h = counts.cpu().numpy()
+        t_co = time.perf_counter()
+
+        # host post-processing (CC.py:316-387)
+        iij = I_full.cpu().numpy().astype(self._dtype) if keep else None
+        for k, K in enumerate(Ks):
+            hist, cdf, bin_edges, pac_area = post.cdf_from_counts(
+                post.pair_counts_to_hist_counts(counts_h[k], n), self.PAC_interval)
+            res = dict(consensus_labels=[], hist=hist, cdf=cdf, bin_edges=bin_edges,
+                       pac_area=pac_area)
+            if keep:
+                res['mij'] = M_full[k].cpu().numpy().astype(self._dtype)
+                res['iij'] = iij
+                res['cij'] = engine.consensus(M_full[k], I_full).cpu().numpy()
+            else:
+                res['mij'] = res['iij'] = res['cij'] = None
+            self.cdf_at_K_data[K] = res
+        self.pair_counts_ = {K: counts_h[k] for k, K in enumerate(Ks)}
+        self.resampling_indices_ = idx
+        self.labels_ = labels  # device uint8 [nK, n, Hpad]; 0xFF = not sampled
+        self._finish_selection()
+        self.timings_ = dict(resample=t_rs - t_start, cluster=t_cl - t_rs,
+                             coassoc=t_co - t_cl, post=time.perf_counter() - t_co,
+                             total=time.perf_counter() - t_start)
+        if self.plot_cdf and rank == 0:
+            self._plot_cdf()
+        return self
+
+    def _finish_selection(self):
+        d = self.cdf_at_K_data
+        self.pac_area_ = {K: float(v['pac_area']) for K, v in d.items()}
+        self.cdf_area_ = {K: post.cdf_area(v['cdf'], v['bin_edges']) for K, v in d.items()}
+        self.delta_k_ = post.delta_k(self.cdf_area_)
+        self.best_k_ = post.best_k(self.pac_area_)
+
+    # ------------------------------------------------------------------ extras
+    def consensus_matrix(self, K):
+        """float32 C for one K (computed on demand on the GPU when not kept)."""
+        v = self.cdf_at_K_data[K]
+        if v.get('cij') is not None:
+            return v['cij']
+        raise ValueError("consensus matrices were not kept (keep_matrices=False)")
+
+    def predict(self, K=None):
+        """Consensus labels: average-linkage agglomerative clustering of 1 - C for K
+        (default best_k_).  The reference's `_get_consensus_labels` (CC.py:292-314) is
+        dead code that no longer runs on sklearn >= 1.4; this uses the same linkage on
+        the precomputed consensus distance."""
+        from sklearn.cluster import AgglomerativeClustering
+
+        K = self.best_k_ if K is None else K
+        C = self.consensus_matrix(K)
+        agg = AgglomerativeClustering(n_clusters=K, metric='precomputed',
+                                      linkage=self.agg_clustering_linkage)
+        return agg.fit_predict(1.0 - C.astype(np.float64))
+
+    def _plot_cdf(self):
+        """CC.py:389-410 (presentation only)."""
+        try:
+            import matplotlib.pyplot as plt
+        except ImportError:  # pragma: no cover
+            return
+        plt.figure(figsize=(4, 4), dpi=120)
+        for K, data in self.cdf_at_K_data.items():
+            x = data['bin_edges']
+            y = [0] + [v for v in data['cdf']]
+            plt.plot(x, y, marker='o', markersize=2.5, label=f'K: {K}', linewidth=2.0)
+        plt.vlines(self.PAC_interval, *plt.ylim(), colors='k', linestyles='dashed', lw=1.5)
+        plt.xlabel('consensus index value')
+        plt.ylabel('CDF')
+        plt.legend()
+        plt.tight_layout()
+        plt.show()
+
+
+def _prepare(X, dev):
+    from .kmeans import prepare_rows
+
+    return prepare_rows(np.asarray(X, dtype=np.float64) if X.dtype.kind != 'f' else X, dev)

@@ -12,11 +12,11 @@
  * (/root/reference/consensus_clustering_parallelised.py, "CC.py" below):
  *
  *   cc_resample_indices   CC.py:216-241  _get_subsampling_indices (numpy RandomState replay)
- *   cc_kpp_first_pos      sklearn _kmeans.py:225 first k-means++ centre (RandomState.choice with p)
  *   cc_scatter_labels     CC.py:260-262, :284-285  indicator / one-hot row placement
  *   cc_cosample           CC.py:264  I = S^T S            (int8 MFMA, upper-triangle tiles)
  *   cc_coassoc            CC.py:287-290 + :338-344  M += L^T L fused with the 20-bin histogram
  *   cc_consensus          CC.py:372-373  C = f32(M) / f32(I + 1e-6), diag 1
+ *   cc_kmeans_plan        packing of the (K, init) problems of one resample into workgroups
  *   cc_kmeans_batched     CC.py:282 clusterer.fit_predict for every (h, K) at once
  *                         (sklearn KMeans: k-means++ init, Lloyd, best of n_init)
  */
@@ -87,31 +87,47 @@ int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int K, int64_t
 /* C = f32(M) / f32(f64(I) + 1e-6) with C_ii = 1 (CC.py:372-373), [n][n]. */
 int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stream);
 
-/* Batched k-means for every (resample h, K, init) problem (sklearn KMeans
- * semantics: k-means++ with 2+floor(ln K) local trials, Lloyd with strict/tol
- * convergence and empty-cluster relocation, best of n_init).
+/* Batched k-means for every (resample h, K, init) problem, replacing the per-(K, h)
+ * clusterer.fit_predict(X[indices]) of CC.py:282 for the default clusterer
+ * (sklearn KMeans: k-means++ init with 2+floor(ln K) local trials, Lloyd with strict
+ * and tol convergence, empty-cluster relocation, best of n_init;
+ * sklearn/cluster/_kmeans.py:174-262, :624-752, :1427-1556).
  *
- *  X        [n][ldx] float32, mean-centred, zero-padded to dpad columns (device)
- *  xnorm    [n] float32 squared row norms of X (device)
- *  idx_hm   [H][m] int32 resample rows (device); problems use h in [h_begin, h_end)
- *  Ks       [nK] K values (host)
- *  kpp_u    [nK][n_init][1 + (Kmax-1)*ntrials_max] doubles: per-(K,init) uniforms of
- *           RandomState(seed) (entry 0 unused; first centre given by kpp_pos) (device)
- *  kpp_pos  [nK][n_init] int32 first-centre row positions (device)
- *  labels_nh  [nK][n][ldl] int8 output, pre-filled 0xFF (device)
- *  inertia  optional [nK][H] float32 best inertia (device) ; n_iter optional [nK][H] int32
- *  stats    optional [4] uint64 (device, accumulated): {lloyd row-centroid dots,
- *           seeding row-candidate dots, sweeps, relocations}
- *  workspace / ws_bytes: from cc_kmeans_workspace_bytes with the same arguments. */
-size_t cc_kmeans_workspace_bytes(int n, int dpad, int H, int m, const int32_t* Ks, int nK,
-                                 int n_init, int h_begin, int h_end);
-int cc_kmeans_batched(const float* X, const float* xnorm, int n, int dpad, int ldx,
+ * Problems are packed into GROUPS (cc_kmeans_plan): every (K, init) of a group shares
+ * one resample's rows, so one workgroup runs a whole group for one resample and reads
+ * each row once per sweep for all of the group's centroids (<= CC_KM_CMAX columns).
+ * Group descriptor g (int32, CC_KM_GSTRIDE entries): [0] = P, then per problem p:
+ * [1+4p] = K, [2+4p] = kidx (index into Ks), [3+4p] = init, [4+4p] = local trials. */
+#define CC_KM_PMAX 64
+#define CC_KM_CMAX 128
+#define CC_KM_GSTRIDE (1 + 4 * CC_KM_PMAX)
+
+/* Pack the (K, n_init) units of Ks[0..nK) into groups; returns the group count (> 0) or a
+ * negative error.  groups must hold max_groups * CC_KM_GSTRIDE int32. */
+int cc_kmeans_plan(const int32_t* Ks, int nK, int n_init, int32_t* groups, int max_groups);
+
+/* Workspace bytes for one cc_kmeans_batched launch over nh resamples. */
+size_t cc_kmeans_workspace_bytes(int m, const int32_t* groups_host, int nG, int nh);
+
+/*  X         [n][dpad] float32, mean-centred, zero-padded from dreal to dpad in {32,64,128}
+ *  xnorm     [n] float32 squared row norms of X
+ *  idx_hm    [H][m] int32 resample rows; this launch runs resamples [h_begin, h_end)
+ *  groups    device copy of the plan; groups_host the same array on the host
+ *  kpp_u     [nK][n_init][kpp_stride] float64: the RandomState(seed) doubles of each
+ *            (K, init) k-means++ run (entry 0: the first-centre draw, consumed on the host)
+ *  kpp_pos   [nK][n_init] int32 first-centre positions in resample order
+ *  labels_nh [nK][n][ldl] uint8 output (pre-filled 0xFF); labels_nh[k][idx[h][r]][h]
+ *  inertia   optional [nK][H] float32; n_iter optional [nK][H] int32
+ *  stats     optional [4] uint64 accumulated: {Lloyd row x centroid products,
+ *            seeding row x candidate products, Lloyd sweeps, relocations}
+ *  All device pointers except groups_host. */
+int cc_kmeans_batched(const float* X, const float* xnorm, int n, int dreal, int dpad,
                       const int32_t* idx_hm, int H, int m, int h_begin, int h_end,
-                      const int32_t* Ks, int nK, int n_init, int max_iter, double tol_rel,
-                      const double* kpp_u, int kpp_stride, const int32_t* kpp_pos,
-                      int8_t* labels_nh, int ldl, float* inertia, int32_t* n_iter,
-                      unsigned long long* stats, void* workspace, size_t ws_bytes,
-                      void* stream);
+                      const int32_t* groups, const int32_t* groups_host, int nG, int n_init,
+                      int max_iter, double tol_rel, const double* kpp_u, int kpp_stride,
+                      const int32_t* kpp_pos, uint8_t* labels_nh, int ldl, float* inertia,
+                      int32_t* n_iter, unsigned long long* stats, void* workspace,
+                      size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }
