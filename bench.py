@@ -1,0 +1,225 @@
+"""Consensus-fit benchmark (BASELINE.json metric) on 1..N MI355X GPUs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One STEP is one full ``ConsensusClustering.fit`` of the workload (all K, all H
+resamples: resampling, batched k-means, co-sampling, co-association + histogram,
+host CDF/PAC), with X already resident in HBM.  Default workload = BASELINE config 3
+(the metric's own: synthetic blobs n=50k, d=128, K=2..20, H=1000, subsampling 0.8),
+strong scaling: the ranks split the fixed fit (resamples for k-means, triangle tiles
+for co-association).  Rank 0 prints ONE JSON line.
+
+``roofline`` is the dominant kernel (cc_kmeans_batched, f32 MFMA-bound): ALGORITHMIC
+flops (2·d per row×centroid distance product of Lloyd and k-means++, + d per M-step row
+update; the kernel counts them) ÷ the launches' HIP-event durations on the launch
+stream, against the 157.3 TF f32 MFMA peak.  ``cpu_baseline`` times the oracle (numpy +
+scikit-learn, the reference's algorithm) on a bounded sample of the same workload on
+this host and extrapolates to resample-clusterings/s (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "consensus fit wall-time + resample-clusterings/sec, n=50k d=128, 1/2/4/8 GPU"
+CONFIGS = {
+    # BASELINE.json configs[2]: the metric's workload
+    "c3": dict(n=50_000, d=128, k_true=8, Ks=list(range(2, 21)), H=1000, frac=0.8),
+    # BASELINE.json configs[1] / configs[4] (d <= 128 paths), for ad-hoc runs
+    "c2": dict(n=10_000, d=64, k_true=6, Ks=list(range(2, 16)), H=500, frac=0.8),
+    "c5": dict(n=200_000, d=32, k_true=6, Ks=list(range(2, 11)), H=256, frac=0.8),
+    "smoke": dict(n=4_000, d=32, k_true=5, Ks=list(range(2, 8)), H=64, frac=0.8),
+}
+F32_MFMA_PEAK_TF = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+SEED = 0
+
+
+def make_blobs_f32(n, d, k, seed=0):
+    """sklearn.datasets.make_blobs(n, d, centers=k, cluster_std=1, center_box=(-10, 10),
+    shuffle=True, random_state=seed) cast to float32."""
+    from sklearn.datasets import make_blobs
+
+    X, _ = make_blobs(n_samples=n, n_features=d, centers=k, cluster_std=1.0,
+                      center_box=(-10.0, 10.0), shuffle=True, random_state=seed)
+    return X.astype(np.float32)
+
+
+def cpu_baseline(cfg, X, budget_s=25.0):
+    """Reference algorithm (oracle: numpy + sklearn) on a bounded sample, extrapolated.
+
+    Per (h, K) the reference does a KMeans fit of X[idx_h] (CC.py:282) and the one-hot
+    co-association M += LᵀL on n x n uint16 (CC.py:284-290).  We time fits for a few K and
+    LᵀL + add on a row block of the n x n product, then extrapolate linearly in K and in
+    rows: T(h,K) = t_fit(K) + t_coassoc(K); T = Σ_K H·T(h,K).
+    """
+    from threadpoolctl import threadpool_limits
+
+    from oracle import cc_oracle as O
+
+    n, H = cfg["n"], cfg["H"]
+    m = int(cfg["frac"] * n)
+    Ks = cfg["Ks"]
+    cores = min(16, os.cpu_count() or 1)
+    idx = O.subsampling_indices(n, 1, cfg["frac"], SEED)
+    sampleK = sorted({Ks[0], Ks[len(Ks) // 2], Ks[-1]})
+    t_fit, t_co = {}, {}
+    block = min(n, 2000)
+    t0 = time.perf_counter()
+    with threadpool_limits(cores):
+        for K in sampleK:
+            a = time.perf_counter()
+            lab = O.kmeans_labels(X[idx[0]], K, SEED, n_init=3)
+            t_fit[K] = time.perf_counter() - a
+            L = np.zeros((K, n), dtype=np.uint16)
+            L[lab, idx[0]] = 1
+            Mblk = np.zeros((block, n), dtype=np.uint16)
+            a = time.perf_counter()
+            mij = np.dot(L[:, :block].T, L)   # CC.py:287 on a row block
+            Mblk += mij                        # CC.py:290
+            t_co[K] = (time.perf_counter() - a) * (n / block)
+            if time.perf_counter() - t0 > budget_s:
+                break
+    done = sorted(t_fit)
+    per_K = {K: np.interp(K, done, [t_fit[k] + t_co[k] for k in done]) for K in Ks}
+    total = H * sum(per_K.values())
+    return {
+        "value": H * len(Ks) / total,
+        "unit": "resample-clusterings/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": (f"oracle (numpy + sklearn {__import__('sklearn').__version__} KMeans n_init=3) "
+                   f"on resample 0 for K in {done}: KMeans fit + one-hot LᵀL/add on a {block}-row "
+                   f"block of the {n}x{n} uint16 M, scaled x{n / block:.0f} in rows, "
+                   f"interpolated over K={Ks[0]}..{Ks[-1]}, x H={H}; extrapolated fit "
+                   f"{total / 3600:.1f} h; sampled {time.perf_counter() - t0:.1f} s"),
+    }
+
+
+def load_traffic(prefix="profiles"):
+    """Per-launch HBM bytes of cc_kmeans_batched from a committed PMC summary, if present."""
+    path = os.path.join(ROOT, prefix, "kmeans_traffic.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f).get("bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from consensus_clustering_amd import ConsensusClustering, engine
+
+    X = make_blobs_f32(cfg["n"], cfg["d"], cfg["k_true"], seed=SEED)
+    Xd = torch.from_numpy(X).to(dev)  # inputs resident in HBM before the timed region
+    cc = ConsensusClustering(K_range=cfg["Ks"], n_iterations=cfg["H"], subsampling=cfg["frac"],
+                             random_state=SEED, plot_cdf=False, keep_matrices=False)
+
+    def barrier():
+        if world > 1:
+            tdist.barrier()
+
+    for _ in range(args.warmup):
+        cc.fit(Xd)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    engine.TIMERS = {}
+    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cc.fit(Xd)
+        stats += cc.kmeans_stats_
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timers = engine.timer_summary(engine.TIMERS)
+    engine.TIMERS = None
+
+    # max over ranks (wall) and sums over ranks (work, kernel time)
+    vec = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    st = stats.to(torch.float64)
+    km_launch, km_ms = timers.get("cc_kmeans_batched", (0, 0.0))
+    ktime = torch.tensor([km_ms, float(km_launch)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tdist.all_reduce(vec, op=tdist.ReduceOp.MAX)
+        tdist.all_reduce(st, op=tdist.ReduceOp.SUM)
+        tdist.all_reduce(ktime, op=tdist.ReduceOp.SUM)
+    elapsed = float(vec[0])
+    d = cfg["d"]
+    flops = 2.0 * d * (float(st[0]) + float(st[1])) + d * float(st[2])
+    km_ms_tot, km_launches = float(ktime[0]), max(float(ktime[1]), 1.0)
+    achieved = flops / (km_ms_tot * 1e-3) / 1e12 if km_ms_tot > 0 else 0.0
+    clusterings = cfg["H"] * len(cfg["Ks"]) * args.steps
+    value = clusterings / elapsed
+
+    if rank == 0:
+        traffic = load_traffic()
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "resample-clusterings/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32 (k-means MFMA) / i8 (co-association MFMA)",
+            "data": "synthetic (make_blobs, float32, seed 0)",
+            "config": {"workload": (f"{args.config}: blobs n={cfg['n']} d={d} k_true={cfg['k_true']}, "
+                                    f"K={cfg['Ks'][0]}..{cfg['Ks'][-1]}, H={cfg['H']}, "
+                                    f"subsampling={cfg['frac']}, n_init=3, full consensus fit"),
+                       "n": cfg["n"], "d": d, "K_range": [cfg["Ks"][0], cfg["Ks"][-1]],
+                       "H": cfg["H"], "parallelism": f"resamples+triangle sharded over {world} GPU(s)"},
+            "roofline": {
+                "kernel": "cc_kmeans_batched",
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": F32_MFMA_PEAK_TF,
+                "unit": "TFLOP/s",
+                "frac": achieved / F32_MFMA_PEAK_TF,
+                "traffic": traffic,
+                "flops_per_launch": flops / km_launches,
+                "avg_launch_ms": km_ms_tot / km_launches,
+            },
+            "kernels_ms_per_step": {k: v[1] / args.steps for k, v in timers.items()},
+            "kernel_launches_per_step": {k: v[0] / args.steps for k, v in timers.items()},
+            "fit_timings_s": {k: round(v, 4) for k, v in cc.timings_.items()},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg, X)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

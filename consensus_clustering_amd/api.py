@@ -133,7 +133,11 @@ class ConsensusClustering:
     def fit(self, X):
         """Fit on X [n_samples, n_features] and fill ``cdf_at_K_data`` (CC.py:92-136)."""
         t_start = time.perf_counter()
-        X = np.asarray(X)
+        if isinstance(X, torch.Tensor):  # already resident in device memory
+            wdtype = np.float64 if X.dtype == torch.float64 else np.float32
+        else:
+            X = np.asarray(X)
+            wdtype = X.dtype if X.dtype in (np.float32, np.float64) else np.float64
         self._N, _ = X.shape
         self._dtype = np.uint8 if self.n_iterations < 256 else np.uint16
         self.cdf_at_K_data = dict()
@@ -163,11 +167,12 @@ class ConsensusClustering:
                                workspace_budget=self.workspace_budget)
             self.kmeans_inertia_ = torch.zeros((len(Ks), H), dtype=torch.float32, device=dev)
             self.kmeans_n_iter_ = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
-            bk.run(Xd, xnorm, X.shape[1], idx_d, n, H, m, h0, h1, labels,
-                   weight_dtype=X.dtype if X.dtype in (np.float32, np.float64) else np.float64,
+            bk.run(Xd, xnorm, X.shape[1], idx_d, n, H, m, h0, h1, labels, weight_dtype=wdtype,
                    inertia=self.kmeans_inertia_, n_iter=self.kmeans_n_iter_)
             self.kmeans_stats_ = bk.stats
         elif Ks:
+            if isinstance(X, torch.Tensor):
+                X = X.cpu().numpy()
             for k, K in enumerate(Ks):
                 self._K = K
                 self._set_clusterer_K()
@@ -276,4 +281,6 @@ class ConsensusClustering:
 def _prepare(X, dev):
     from .kmeans import prepare_rows
 
-    return prepare_rows(np.asarray(X, dtype=np.float64) if X.dtype.kind != 'f' else X, dev)
+    if not isinstance(X, torch.Tensor) and X.dtype.kind != 'f':
+        X = np.asarray(X, dtype=np.float64)
+    return prepare_rows(X, dev)

@@ -97,7 +97,7 @@ struct State {
   int red_i[NT / 64];
   int P, ncols, colmask, any, flag, Kg;
   float tol;
-  unsigned long long n_lloyd, n_seed, n_sweeps, n_reloc;
+  unsigned long long n_lloyd, n_seed, n_mrows, n_reloc;
 };
 
 template <int DP>
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       kg = max(kg, S.K[p]);
     }
     S.Kg = kg;
-    S.n_lloyd = S.n_seed = S.n_sweeps = S.n_reloc = 0;
+    S.n_lloyd = S.n_seed = S.n_mrows = S.n_reloc = 0;
   }
   __syncthreads();
   const int P = S.P;
@@ -534,21 +534,20 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     if (tid == 0) {
       unsigned msk = 0;
       int any = 0;
-      unsigned long long work = 0;
+      unsigned long long work = 0, mrows = 0;
       for (int p = 0; p < P; ++p) {
         const int st = S.st[p];
         if (st == ST_RUN || st == ST_FINAL) {
           any = 1;
           for (int ct = S.off[p] / 32; ct <= (S.off[p] + S.K[p] - 1) / 32; ++ct) msk |= 1u << ct;
           work += static_cast<unsigned long long>(S.K[p]) * m;
+          if (st == ST_RUN) mrows += m;
         }
       }
       S.colmask = static_cast<int>(msk);
       S.any = any;
-      if (any) {
-        S.n_lloyd += work;
-        S.n_sweeps += 1;
-      }
+      S.n_lloyd += work;
+      S.n_mrows += mrows;
     }
     if (tid < CMAX) S.cnt[tid] = 0;
     if (tid < PMAX) S.changed[tid] = 0;
@@ -801,7 +800,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
   if (tid == 0 && a.stats) {
     atomicAdd(&a.stats[0], S.n_lloyd);
     atomicAdd(&a.stats[1], S.n_seed);
-    atomicAdd(&a.stats[2], S.n_sweeps);
+    atomicAdd(&a.stats[2], S.n_mrows);
     atomicAdd(&a.stats[3], S.n_reloc);
   }
 }

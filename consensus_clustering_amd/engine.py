@@ -33,6 +33,35 @@ def stream_ptr(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+# Optional per-launch HIP-event timing (bench.py): {kernel name: [(start, end), ...]}.
+TIMERS = None
+
+
+class timed:
+    """Record HIP events around a launch on the current stream when TIMERS is enabled."""
+
+    def __init__(self, name):
+        self.name = name
+        self.ev = None
+
+    def __enter__(self):
+        if TIMERS is not None:
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ev is not None:
+            self.ev[1].record()
+            TIMERS.setdefault(self.name, []).append(self.ev)
+        return False
+
+
+def timer_summary(timers) -> dict:
+    """{name: (launches, total ms)} after a synchronize."""
+    return {k: (len(v), sum(a.elapsed_time(b) for a, b in v)) for k, v in timers.items()}
+
+
 def pad_h(H: int) -> int:
     return ((H + HALIGN - 1) // HALIGN) * HALIGN
 
@@ -96,8 +125,9 @@ def cosample(labels_nh: torch.Tensor, n: int, Hpad: int, tile_begin: int, tile_e
     ntl = tile_end - tile_begin
     I_tiles = torch.empty((max(ntl, 0), TILE * TILE), dtype=torch.int16, device=dev)
     I_full = torch.zeros((n, n), dtype=torch.int32, device=dev) if want_full else None
-    _lib.call("cc_cosample", labels_nh.data_ptr(), n, labels_nh.stride(0), Hpad, tile_begin,
-              tile_end, I_tiles.data_ptr(), _lib.ptr(I_full), stream_ptr())
+    with timed("cc_cosample"):
+        _lib.call("cc_cosample", labels_nh.data_ptr(), n, labels_nh.stride(0), Hpad, tile_begin,
+                  tile_end, I_tiles.data_ptr(), _lib.ptr(I_full), stream_ptr())
     return I_tiles, I_full
 
 
@@ -110,9 +140,10 @@ def coassoc(labels_nh: torch.Tensor, n: int, Hpad: int, K: int, tile_begin: int,
             M_full: torch.Tensor = None):
     """Accumulate the strict-upper-pair histogram of C for one K into counts (int64[20])."""
     assert counts.dtype == torch.int64 and counts.numel() == N_BINS
-    _lib.call("cc_coassoc", labels_nh.data_ptr(), n, labels_nh.stride(0), Hpad, int(K),
-              tile_begin, tile_end, I_tiles.data_ptr(), edges.data_ptr(), counts.data_ptr(),
-              _lib.ptr(M_full), stream_ptr())
+    with timed("cc_coassoc"):
+        _lib.call("cc_coassoc", labels_nh.data_ptr(), n, labels_nh.stride(0), Hpad, int(K),
+                  tile_begin, tile_end, I_tiles.data_ptr(), edges.data_ptr(), counts.data_ptr(),
+                  _lib.ptr(M_full), stream_ptr())
 
 
 def consensus(M: torch.Tensor, I: torch.Tensor) -> torch.Tensor:

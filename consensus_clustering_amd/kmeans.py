@@ -59,20 +59,22 @@ def kpp_tables(Ks, n_init: int, seed: int, m: int, weight_dtype=np.float32):
     return u, pos, stride
 
 
-def prepare_rows(X: np.ndarray, device):
+def prepare_rows(X, device):
     """Mean-centred float32 rows zero-padded to dpad, and their squared norms, on device.
 
-    sklearn centres X_sub by its own mean (_kmeans.py:1479-1481); distances are
-    translation invariant, so one global centring serves every resample.
+    X is a host array or a device tensor (already resident in HBM).  sklearn centres
+    X_sub by its own mean (_kmeans.py:1479-1481); distances are translation invariant,
+    so one global centring serves every resample.
     """
     n, d = X.shape
     dpad = next((p for p in DPADS if d <= p), None)
     if dpad is None:
         raise _lib.CCMIError(f"batched k-means supports d <= {DPADS[-1]} in this build (got d={d})")
-    mean = X.mean(axis=0, dtype=np.float64).astype(np.float32)
-    Xc = np.zeros((n, dpad), dtype=np.float32)
-    Xc[:, :d] = X.astype(np.float32) - mean
-    Xd = torch.from_numpy(Xc).to(device)
+    Xt = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X))
+    Xt = Xt.to(device)
+    mean = Xt.to(torch.float64).mean(dim=0).to(torch.float32)
+    Xd = torch.zeros((n, dpad), dtype=torch.float32, device=device)
+    Xd[:, :d] = Xt.to(torch.float32) - mean
     xnorm = (Xd * Xd).sum(dim=1).contiguous()
     return Xd, xnorm, dpad
 
@@ -111,10 +113,11 @@ class BatchedKMeans:
         ldl = labels_nh.stride(1)
         for h0 in range(h_begin, h_end, hb):
             h1 = min(h_end, h0 + hb)
-            _lib.call("cc_kmeans_batched", Xd.data_ptr(), xnorm.data_ptr(), n, int(dreal),
-                      Xd.shape[1], idx_d.data_ptr(), H, m, h0, h1, g_d.data_ptr(),
-                      g_h.ctypes.data, nG, self.n_init, self.max_iter, self.tol,
-                      u_d.data_ptr(), stride, pos_d.data_ptr(), labels_nh.data_ptr(), ldl,
-                      _lib.ptr(inertia), _lib.ptr(n_iter), self.stats.data_ptr(),
-                      ws.data_ptr(), ws.numel(), engine.stream_ptr(dev))
+            with engine.timed("cc_kmeans_batched"):
+                _lib.call("cc_kmeans_batched", Xd.data_ptr(), xnorm.data_ptr(), n, int(dreal),
+                          Xd.shape[1], idx_d.data_ptr(), H, m, h0, h1, g_d.data_ptr(),
+                          g_h.ctypes.data, nG, self.n_init, self.max_iter, self.tol,
+                          u_d.data_ptr(), stride, pos_d.data_ptr(), labels_nh.data_ptr(), ldl,
+                          _lib.ptr(inertia), _lib.ptr(n_iter), self.stats.data_ptr(),
+                          ws.data_ptr(), ws.numel(), engine.stream_ptr(dev))
         return labels_nh

@@ -118,8 +118,9 @@ size_t cc_kmeans_workspace_bytes(int m, const int32_t* groups_host, int nG, int 
  *  kpp_pos   [nK][n_init] int32 first-centre positions in resample order
  *  labels_nh [nK][n][ldl] uint8 output (pre-filled 0xFF); labels_nh[k][idx[h][r]][h]
  *  inertia   optional [nK][H] float32; n_iter optional [nK][H] int32
- *  stats     optional [4] uint64 accumulated: {Lloyd row x centroid products,
- *            seeding row x candidate products, Lloyd sweeps, relocations}
+ *  stats     optional [4] uint64 accumulated: {Lloyd row x centroid distance products,
+ *            seeding row x candidate distance products, Lloyd M-step row updates
+ *            (rows x running problems), empty-cluster relocations}
  *  All device pointers except groups_host. */
 int cc_kmeans_batched(const float* X, const float* xnorm, int n, int dreal, int dpad,
                       const int32_t* idx_hm, int H, int m, int h_begin, int h_end,
