@@ -122,8 +122,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--H", type=int, default=None, help="override n_iterations (debug runs)")
     args = ap.parse_args()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.H:
+        cfg["H"] = args.H
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -144,17 +147,20 @@ def main():
         if world > 1:
             tdist.barrier()
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         cc.fit(Xd)
+        print(f"[bench] warmup {i}: {cc.timings_}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     engine.TIMERS = {}
-    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    stats = torch.zeros(64, dtype=torch.int64, device=dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         cc.fit(Xd)
         stats += cc.kmeans_stats_
+        if rank == 0:
+            print(f"[bench] step {i} queued", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

@@ -2,8 +2,8 @@
 //
 // Replaces the per-(K, h) `clusterer.fit_predict(X[indices])` of the reference
 // (consensus_clustering_parallelised.py:282, default clusterer KMeans(), CC.py:88-90,
-// with set_params(random_state=seed, n_init=3), CC.py:212-214) by ONE launch over all
-// problems.  The algorithm is scikit-learn's KMeans (sklearn/cluster/_kmeans.py):
+// with set_params(random_state=seed, n_init=3), CC.py:212-214) by launches that run
+// every problem at once.  The algorithm is scikit-learn's KMeans (sklearn/cluster/_kmeans.py):
 //   * k-means++ seeding (:174-262): first centre from RandomState(seed).choice with
 //     uniform p (resolved on the host), then per centre 2+floor(ln K) candidates drawn
 //     by searchsorted(cumsum(closest d^2), u * pot), the candidate minimising the
@@ -15,20 +15,22 @@
 //     a final E-step when not strictly converged;
 //   * best of n_init: lower inertia AND a different clustering (:1525-1531).
 //
-// Mapping.  A workgroup (512 threads, 8 waves, ~142 KiB LDS) owns one resample h and
-// one GROUP of problems (<= 128 centroid columns, <= 64 problems; all n_init runs of a
-// K in one group).  It runs the whole fit of every problem of the group on-chip: the
-// resample's rows stream through LDS in 64-row tiles, once per sweep for ALL the
-// group's centroids, so X is read once per sweep per group instead of once per
-// problem.  Per tile:
-//   distances   D = cnorm - 2 * C.X^T on v_mfma_f32_32x32x2_f32 (exact f32 fma
-//               chain), centroids and rows from LDS by ds_read_b128; the 8 waves own
-//               (row-half, 32-column tile) work items;
-//   argmin      one wave per problem, one lane per row, counts by wave ballots;
-//   M-step sums S += onehot(labels)^T . X on the same f32 MFMA (0/1 operand: exact
-//               products, deterministic order), accumulators resident in registers for
-//               the whole sweep.
-// Nothing crosses workgroups, so the result is independent of scheduling and of how
+// Mapping.  A workgroup (512 threads, ~145 KiB LDS, one per CU) owns one resample h and
+// one GROUP of problems (<= 128 centroid columns, <= 32 problems; all n_init runs of a
+// K in one group) and runs their whole fits on-chip.  The resample's rows stream
+// through LDS in 32-row tiles, once per sweep for ALL the group's centroids.  The 8
+// waves are specialised, one of each kind per SIMD:
+//   MFMA waves (0-3)  wave w owns centroid columns 32w..32w+31 as register-resident
+//                     A fragments and computes D = |c|^2 - 2 c.x for the tile on
+//                     v_mfma_f32_32x32x2_f32 (exact f32 fma chain);
+//   VALU waves (4-7)  gather the next tile's rows into LDS, run the E-step of the
+//                     previous tile (argmin per row and problem: strict <, lowest
+//                     index) and its M-step (per-(column, dim) owner threads add the
+//                     rows into LDS sums with ds_add_f32: one owner per address, rows
+//                     in order -> deterministic sums).
+// The two kinds overlap through a 3-deep tile ring with two workgroup barriers per
+// tile: tile t's distances (MFMA) run beside tile t-1's E/M-steps and tile t+1's gather.
+// Nothing crosses workgroups, so results do not depend on scheduling or on how the
 // resamples are sharded over launches or GPUs.
 #include <hip/hip_runtime.h>
 
@@ -43,11 +45,14 @@
 namespace {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NT = 512;
 constexpr int NW = 8;
-constexpr int RT = 64;              // rows per tile
-constexpr int CMAX = CC_KM_CMAX;    // 128 centroid / candidate columns
+constexpr int NVT = 256;            // VALU-role threads (waves 4..7)
+constexpr int RT = 32;              // rows per tile (one MFMA row block)
+constexpr int CMAX = CC_KM_CMAX;    // 128 centroid / candidate columns (4 MFMA waves x 32)
 constexpr int PMAX = CC_KM_PMAX;    // 64 problems per group
 constexpr int TMAX = 6;             // max local trials: 2 + floor(ln 127)
 constexpr int DSD = CMAX + 1;       // distance-tile row stride (floats)
@@ -88,13 +93,14 @@ struct State {
   double sweep_inert[PMAX];
   int cand[PMAX][TMAX];
   short colprob[CMAX], coltr[CMAX];
+  int colrow[CMAX];  // source row of each MFMA column (seeding candidates / initial centres)
   unsigned cnt[CMAX];
   float cnorm[CMAX], shift[CMAX];
-  double potc[CMAX];
-  float xn[RT];
+  double potc[CMAX], potc2[CMAX];
+  float xn[3][RT];
   int map[KMAX + 1];
-  double red_v[NT / 64];
-  int red_i[NT / 64];
+  double red_v[NW];
+  int red_i[NW];
   int P, ncols, colmask, any, flag, Kg;
   float tol;
   unsigned long long n_lloyd, n_seed, n_mrows, n_reloc;
@@ -102,16 +108,16 @@ struct State {
 
 template <int DP>
 struct Lay {
-  static constexpr int DS = DP + 4;  // LDS row stride of centroid / row / sum tiles (floats)
-  static constexpr int CS_BYTES = CMAX * DS * 4;
-  static constexpr int XS_BYTES = RT * DS * 4;
-  static constexpr int DD_BYTES = RT * DSD * 4;
-  static constexpr int U_BYTES = (XS_BYTES + DD_BYTES > CS_BYTES) ? XS_BYTES + DD_BYTES : CS_BYTES;
-  static constexpr int OFF_U = CS_BYTES;
-  static constexpr int OFF_LS = OFF_U + U_BYTES;
-  static constexpr int OFF_ST = OFF_LS + PMAX * RT;
+  static constexpr int XS = DP + 4;            // X tile row stride (floats): conflict-free b128 reads
+  static constexpr int XBUF = RT * XS;         // floats per X ring slot
+  static constexpr int OFF_D = 3 * XBUF * 4;   // distance tile [RT][DSD]
+  static constexpr int U_END = OFF_D + RT * DSD * 4;
+  static constexpr int S_BYTES = CMAX * DP * 4;      // sums / new centres, aliasing the ring
+  static_assert(S_BYTES <= U_END, "centre sums must fit in the tile ring");
+  static constexpr int OFF_CO = (U_END + 15) / 16 * 16;  // old centres [CMAX][DP]
+  static constexpr int OFF_LS = OFF_CO + S_BYTES;        // tile labels [PMAX][RT]
+  static constexpr int OFF_ST = OFF_LS + RT * PMAX;
   static constexpr int TOTAL = OFF_ST + ((sizeof(State) + 15) / 16) * 16;
-  static constexpr int NDT = DP / 32;  // 32-wide dim tiles of the M-step GEMM
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -120,63 +126,24 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// 64 resample rows [r0, r0+64) -> Xs (zero-padded past m) and their squared norms.
-template <int DP>
-__device__ __forceinline__ void load_tile(const KArgs& a, const int32_t* idx, int r0, float* Xs,
-                                          State& S, int tid) {
-  using LY = Lay<DP>;
-  constexpr int NV = DP / 4;
-  constexpr int PER = RT * NV / NT;
+__device__ __forceinline__ double half_sum(double v) {  // over the 32 lanes of a half-wave
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int e = tid + NT * i;
-    const int row = e / NV, c4 = e - (e / NV) * NV;
-    const int r = r0 + row;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < a.m) v = *reinterpret_cast<const float4*>(a.X + static_cast<size_t>(idx[r]) * a.ldx + 4 * c4);
-    *reinterpret_cast<float4*>(Xs + row * LY::DS + 4 * c4) = v;
-  }
-  if (tid < RT) {
-    const int r = r0 + tid;
-    S.xn[tid] = r < a.m ? a.xnorm[idx[r]] : 0.f;
-  }
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
 }
 
-// Ds[row][col] = cnorm[col] - 2 * <C[col], X[row]> for the 32-column tiles set in mask.
-// Work item of wave w: rows (w & 1) * 32 .. +32, columns (w >> 1) * 32 .. +32.
-template <int DP>
-__device__ __forceinline__ void dist_phase(const float* Cs, const float* Xs, const State& S,
-                                           float* Ds, unsigned mask, int wave, int lane) {
-  using LY = Lay<DP>;
-  const int rs = wave & 1, ct = wave >> 1;
-  if (!((mask >> ct) & 1u)) return;
-  const float* ap = Cs + (ct * 32 + (lane & 31)) * LY::DS + 4 * (lane >> 5);
-  const float* bp = Xs + (rs * 32 + (lane & 31)) * LY::DS + 4 * (lane >> 5);
-  v16f acc = {};
-#pragma unroll
-  for (int s = 0; s < DP / 8; ++s) {
-    const float4 av = *reinterpret_cast<const float4*>(ap + 8 * s);
-    const float4 bv = *reinterpret_cast<const float4*>(bp + 8 * s);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
-  }
-  float* drow = Ds + (rs * 32 + (lane & 31)) * DSD + ct * 32 + 4 * (lane >> 5);
-#pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const int i = (v & 3) + 8 * (v >> 2);
-    drow[i] = S.cnorm[ct * 32 + 4 * (lane >> 5) + i] - 2.0f * acc[v];
-  }
-}
-
-// sum of squares of a centroid row (sklearn row_norms: f32, sequential).
-template <int DP>
-__device__ __forceinline__ float row_sq(const float* c, int dreal) {
-  float s = 0.f;
-  for (int d = 0; d < dreal; ++d) s = fmaf(c[d], c[d], s);
-  return s;
-}
+// Diagnostic build only (-DCC_KM_STAMPS): per-wave cycle accounting of the Lloyd sweep
+// phases of workgroup 0, added into stats[4 + 4*wave + k] (k: work1, wait1, work2, wait2).
+#ifdef CC_KM_STAMPS
+#define KM_STAMP(var) \
+  __builtin_amdgcn_sched_barrier(0); \
+  const unsigned long long var = __builtin_amdgcn_s_memtime(); \
+  __builtin_amdgcn_sched_barrier(0)
+#define KM_ACC(k, a, b) st_acc[k] += (b) - (a)
+#else
+#define KM_STAMP(var)
+#define KM_ACC(k, a, b)
+#endif
 
 // numpy pairwise_sum of a short contiguous float32 array (n <= 128), as
 // `(center_shift ** 2).sum()` evaluates it (numpy/_core/src/umath/loops_utils.h).
@@ -198,18 +165,134 @@ __device__ __forceinline__ float np_pairwise_sum(const float* a, int n) {
   return res;
 }
 
-// Empty-cluster relocation for problem p (rare path; _k_means_common.pyx:167-212).
-// Sn holds the un-averaged sums, Cs the centres the labels were computed with.
+// sum of squares of a centre row (sklearn row_norms: f32, sequential).
+__device__ __forceinline__ float row_sq(const float* c, int dreal) {
+  float s = 0.f;
+  for (int d = 0; d < dreal; ++d) s = fmaf(c[d], c[d], s);
+  return s;
+}
+
+// ---- VALU-role tile gather: issue the global loads early, commit to LDS late ----
 template <int DP>
-__device__ void relocate(const KArgs& a, const int32_t* idx, int p, float* Cs, float* Sn,
-                         State& S, uint8_t* glab, float* dist, int tid) {
+struct TileRegs {
+  static constexpr int PER = RT * (DP / 4) / NVT;  // float4 per VALU thread (1, 2 or 4)
+  float4 v[PER];
+  float xn;
+};
+
+template <int DP>
+__device__ __forceinline__ void tile_issue(const KArgs& a, const int32_t* idx, int r0, int vt,
+                                           TileRegs<DP>& R) {
+  // Branch-free gather: all row indices first, then all rows (two dependent round trips).
+  constexpr int NV = DP / 4;
+  constexpr int PER = TileRegs<DP>::PER;
+  int src[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int row = (vt + NVT * i) / NV;
+    src[i] = idx[min(r0 + row, a.m - 1)];
+  }
+  const int xr = min(r0 + (vt & (RT - 1)), a.m - 1);
+  const float xn = a.xnorm[idx[xr]];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = vt + NVT * i;
+    const int row = e / NV, c4 = e - (e / NV) * NV;
+    const float4 v = *reinterpret_cast<const float4*>(a.X + static_cast<size_t>(src[i]) * a.ldx + 4 * c4);
+    const bool ok = r0 + row < a.m;
+    R.v[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  R.xn = (r0 + (vt & (RT - 1)) < a.m) ? xn : 0.f;
+}
+
+template <int DP>
+__device__ __forceinline__ void tile_commit(float* Xb, float* xn, int vt, const TileRegs<DP>& R) {
   using LY = Lay<DP>;
+  constexpr int NV = DP / 4;
+#pragma unroll
+  for (int i = 0; i < TileRegs<DP>::PER; ++i) {
+    const int e = vt + NVT * i;
+    const int row = e / NV, c4 = e - (e / NV) * NV;
+    *reinterpret_cast<float4*>(Xb + row * LY::XS + 4 * c4) = R.v[i];
+  }
+  if (vt < RT) xn[vt] = R.xn;
+}
+
+// ---- MFMA-role helpers -------------------------------------------------------
+// Fragment of column (32*ct + lane%32): dims 8s + 4*(lane/32) .. +3 for s < DP/8.
+template <int DP>
+__device__ __forceinline__ void frag_load(float4 (&cf)[DP / 8], const float* src, bool valid, int lane) {
+  const int g4 = 4 * (lane >> 5);
+#pragma unroll
+  for (int s = 0; s < DP / 8; ++s)
+    cf[s] = valid ? *reinterpret_cast<const float4*>(src + 8 * s + g4) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int DP, int S0, int S1>
+__device__ __forceinline__ void mfma_dims(const float4 (&cf)[DP / 8], const float* Xb, v16f& acc, int lane) {
+  using LY = Lay<DP>;
+  const float* bp = Xb + (lane & 31) * LY::XS + 4 * (lane >> 5);
+#pragma unroll
+  for (int s = S0; s < S1; ++s) {
+    const float4 bv = *reinterpret_cast<const float4*>(bp + 8 * s);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf[s].x, bv.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf[s].y, bv.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf[s].z, bv.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf[s].w, bv.w, acc, 0, 0, 0);
+  }
+}
+
+// Ds[row][col] = cnorm[col] - 2 acc  (acc = D[col][row]: lane = row, regs = columns)
+__device__ __forceinline__ void store_dist(const v16f& acc, const State& S, float* Ds, int ct, int lane) {
+  float* drow = Ds + (lane & 31) * DSD + ct * 32 + 4 * (lane >> 5);
+  const float* cn = S.cnorm + ct * 32 + 4 * (lane >> 5);
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const int i = (v & 3) + 8 * (v >> 2);
+    drow[i] = cn[i] - 2.0f * acc[v];
+  }
+}
+
+// ---- M-step on bf16 MFMA: S[col][dim] += sum_rows onehot[col][row] * x[row][dim] ----
+// x = x0 + x1 + x2 with bf16 x0 = RN(x), x1 = RN(x - x0), x2 = RN(x - x0 - x1): the one-hot
+// products are exact and the three bf16 MFMAs add the row's value back to f32 precision.
+__device__ __forceinline__ unsigned bf16_pack(float a, float b) {
+  return static_cast<unsigned>(__builtin_bit_cast(unsigned short, static_cast<__bf16>(a))) |
+         (static_cast<unsigned>(__builtin_bit_cast(unsigned short, static_cast<__bf16>(b))) << 16);
+}
+__device__ __forceinline__ float bf16_lo(unsigned p) { return __builtin_bit_cast(float, p << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned p) { return __builtin_bit_cast(float, p & 0xFFFF0000u); }
+
+// 8 f32 values -> 3 bf16x8 fragments (hi, mid, lo parts)
+__device__ __forceinline__ void split3(const float (&x)[8], u32x4& f0, u32x4& f1, u32x4& f2) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = x[2 * i], b = x[2 * i + 1];
+    const unsigned p0 = bf16_pack(a, b);
+    const float ra = a - bf16_lo(p0), rb = b - bf16_hi(p0);
+    const unsigned p1 = bf16_pack(ra, rb);
+    const unsigned p2 = bf16_pack(ra - bf16_lo(p1), rb - bf16_hi(p1));
+    f0[i] = p0;
+    f1[i] = p1;
+    f2[i] = p2;
+  }
+}
+
+__device__ __forceinline__ v16f mfma_bf16(const u32x4& a, const u32x4& b, const v16f& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// Empty-cluster relocation for problem p (rare path; _k_means_common.pyx:167-212).
+// Sm holds the un-averaged sums [CMAX][DP], Co the centres the labels came from.
+template <int DP>
+__device__ void relocate(const KArgs& a, const int32_t* idx, int p, const float* Co, float* Sm,
+                         State& S, const uint8_t* glab, float* dist, int tid) {
   const int m = a.m, off = S.off[p], K = S.K[p];
-  // distances of every row to its (old) centre, f32 like ((X - C[labels])**2).sum(1)
   float mymax = 0.f;
   for (int r = tid; r < m; r += NT) {
     const float* x = a.X + static_cast<size_t>(idx[r]) * a.ldx;
-    const float* c = Cs + (off + glab[static_cast<size_t>(p) * m + r]) * LY::DS;
+    const float* c = Co + (off + glab[static_cast<size_t>(p) * m + r]) * DP;
     float s = 0.f;
     for (int d = 0; d < a.dreal; ++d) {
       const float t = x[d] - c[d];
@@ -218,14 +301,11 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, float* Cs, f
     dist[r] = s;
     mymax = fmaxf(mymax, s);
   }
-  // block max: 0 => nothing to relocate (sklearn returns early)
   for (int o = 32; o > 0; o >>= 1) mymax = fmaxf(mymax, __shfl_xor(mymax, o));
   if ((tid & 63) == 0) S.red_v[tid >> 6] = mymax;
   __syncthreads();
   double gmax = 0.0;
   for (int w = 0; w < NW; ++w) gmax = fmax(gmax, S.red_v[w]);
-  __syncthreads();
-  if (gmax == 0.0) return;
   // the empty clusters are fixed before any relocation (np.where(weight == 0))
   if (tid == 0) {
     int ne = 0;
@@ -234,10 +314,10 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, float* Cs, f
     S.flag = ne;
   }
   __syncthreads();
+  if (gmax == 0.0) return;  // sklearn returns early when every point sits on its centre
   const int ne = S.flag;
   for (int e = 0; e < ne; ++e) {
     const int c = S.map[e];
-    // far = argmax dist (ties -> lowest row)
     float bv = -1.f;
     int bi = 0x7fffffff;
     for (int r = tid; r < m; r += NT) {
@@ -270,8 +350,8 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, float* Cs, f
     const int old = glab[static_cast<size_t>(p) * m + gi];
     const float* x = a.X + static_cast<size_t>(idx[gi]) * a.ldx;
     for (int d = tid; d < DP; d += NT) {
-      Sn[(off + old) * LY::DS + d] -= x[d];
-      Sn[(off + c) * LY::DS + d] = x[d];
+      Sm[(off + old) * DP + d] -= x[d];
+      Sm[(off + c) * DP + d] = x[d];
     }
     __syncthreads();
     if (tid == 0) {
@@ -287,27 +367,31 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, float* Cs, f
 template <int DP>
 __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
   using LY = Lay<DP>;
-  constexpr int DS = LY::DS;
-  constexpr int NDT = LY::NDT;
   __shared__ __attribute__((aligned(16))) char smem[LY::TOTAL];
-  float* Cs = reinterpret_cast<float*>(smem);
-  float* Xs = reinterpret_cast<float*>(smem + LY::OFF_U);
-  float* Ds = reinterpret_cast<float*>(smem + LY::OFF_U + LY::XS_BYTES);
-  float* Sn = reinterpret_cast<float*>(smem + LY::OFF_U);
+  float* Xr = reinterpret_cast<float*>(smem);                 // 3-slot tile ring
+  float* Ds = reinterpret_cast<float*>(smem + LY::OFF_D);     // distance tile
+  float* Co = reinterpret_cast<float*>(smem + LY::OFF_CO);    // old centres (sweep end)
+  float* Sm = reinterpret_cast<float*>(smem);                 // sums / new centres (aliases ring)
   uint8_t* Ls = reinterpret_cast<uint8_t*>(smem + LY::OFF_LS);
   State& S = *reinterpret_cast<State*>(smem + LY::OFF_ST);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave index made provably uniform, so the role branches below are scalar branches
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool mrole = wave < 4;      // MFMA waves 0-3, VALU waves 4-7 (one of each per SIMD)
+  const int ct = wave;              // MFMA role: centroid column tile
+  const int vt = tid - NVT;         // VALU role: 0..255
   const int g = blockIdx.x / a.nh;  // heavy groups (planned first) dispatch first
   const int hb = blockIdx.x - g * a.nh;
   const int h = a.h_begin + hb;
   const int m = a.m;
+  const int T = (m + RT - 1) / RT;
   const int32_t* idx = a.idx + static_cast<size_t>(h) * m;
   const int32_t* gd = a.groups + g * GS;
   uint8_t* wsb = a.ws + static_cast<size_t>(blockIdx.x) * a.ws_per_wg;
-  uint8_t* glab = wsb;                                                // [Pws][m]
-  float* dbuf = reinterpret_cast<float*>(wsb + a.off_dbuf);           // [Pws][Tws+1][m]
-  int32_t* cpos = reinterpret_cast<int32_t*>(wsb + a.off_cpos);       // [Pws][Kws]
+  uint8_t* glab = wsb;                                           // [Pws][m]
+  float* dbuf = reinterpret_cast<float*>(wsb + a.off_dbuf);      // [Pws][Tws+1][m]
+  int32_t* cpos = reinterpret_cast<int32_t*>(wsb + a.off_cpos);  // [Pws][Kws]
   const int T1 = a.Tws + 1;
 
   // ---- problem table --------------------------------------------------------
@@ -331,8 +415,8 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
 
   // ---- tol = tol_rel * mean(var(X_sub, axis=0)) (sklearn _tolerance, :270-278) --
   {
-    double* red = reinterpret_cast<double*>(Xs);  // [NT/DP][DP]
-    double* mean = reinterpret_cast<double*>(Xs) + NT;
+    double* red = reinterpret_cast<double*>(Xr);  // [NT/DP][DP]
+    double* mean = reinterpret_cast<double*>(Xr) + NT;
     constexpr int NPH = NT / DP;
     const int d = tid % DP, ph = tid / DP;
     double s = 0.0;
@@ -419,6 +503,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         for (int t = 0; t < nt; ++t) {
           S.colprob[j] = static_cast<short>(p);
           S.coltr[j] = static_cast<short>(t);
+          S.colrow[j] = idx[S.cand[p][t]];
           ++j;
         }
       }
@@ -428,59 +513,76 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     }
     __syncthreads();
     const int ncols = S.ncols;
-    const unsigned mask = static_cast<unsigned>(S.colmask);
-    // candidate rows -> Cs, cnorm
-    for (int e = tid; e < CMAX * (DP / 4); e += NT) {
-      const int col = e / (DP / 4), c4 = e - col * (DP / 4);
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (col < ncols) {
-        const int p = S.colprob[col];
-        const int row = idx[S.cand[p][S.coltr[col]]];
-        v = *reinterpret_cast<const float4*>(a.X + static_cast<size_t>(row) * a.ldx + 4 * c4);
+    // Role-split pipeline (same barrier count on both sides): the MFMA waves keep the
+    // candidate fragments live, the VALU waves keep the potential partial live.
+    if (mrole) {
+      float4 cf[DP / 8];
+      const bool active = (S.colmask >> ct) & 1;
+      const int col = ct * 32 + (lane & 31);
+      const bool ok = col < ncols;
+      frag_load<DP>(cf, a.X + static_cast<size_t>(ok ? S.colrow[col] : 0) * a.ldx, ok, lane);
+      __syncthreads();
+      for (int t = 0; t <= T; ++t) {
+        v16f acc = {};
+        if (active && t < T) mfma_dims<DP, 0, DP / 16>(cf, Xr + (t % 3) * LY::XBUF, acc, lane);
+        __syncthreads();
+        if (active && t < T) {
+          mfma_dims<DP, DP / 16, DP / 8>(cf, Xr + (t % 3) * LY::XBUF, acc, lane);
+          store_dist(acc, S, Ds, ct, lane);
+        }
+        __syncthreads();
       }
-      *reinterpret_cast<float4*>(Cs + col * DS + 4 * c4) = v;
-    }
-    if (tid < CMAX) {
-      float cn = 0.f;
-      if (tid < ncols) cn = a.xnorm[idx[S.cand[S.colprob[tid]][S.coltr[tid]]]];
-      S.cnorm[tid] = cn;
-    }
-    __syncthreads();
-    double pacc[CMAX / NW];
-#pragma unroll
-    for (int i = 0; i < CMAX / NW; ++i) pacc[i] = 0.0;
-    for (int r0 = 0; r0 < m; r0 += RT) {
-      load_tile<DP>(a, idx, r0, Xs, S, tid);
+    } else {
+      if (vt < CMAX) S.cnorm[vt] = (vt < ncols) ? a.xnorm[S.colrow[vt]] : 0.f;
+      {
+        TileRegs<DP> R;
+        tile_issue<DP>(a, idx, 0, vt, R);
+        tile_commit<DP>(Xr, S.xn[0], vt, R);
+      }
       __syncthreads();
-      dist_phase<DP>(Cs, Xs, S, Ds, mask, wave, lane);
-      __syncthreads();
-      const int r = r0 + lane;
-      if (r < m) {
-        const float xnr = S.xn[lane];
+      // candidate potentials: thread = (column j, half tile of 16 rows)
+      const int j = vt & (CMAX - 1), rh = vt >> 7;
+      const bool jok = j < ncols;
+      int p = 0, cs = 0, slot = 0;
+      if (jok) {
+        p = S.colprob[j];
+        cs = S.cs[p];
+        const int tr = S.coltr[j];
+        slot = (tr < cs) ? tr : tr + 1;
+      }
+      const float* closest = dbuf + (static_cast<size_t>(p) * T1 + cs) * m;
+      float* dout = dbuf + (static_cast<size_t>(p) * T1 + slot) * m;
+      double pacc = 0.0;
+      for (int t = 0; t <= T; ++t) {
+        int vtl = vt;
+        asm volatile("" : "+v"(vtl));
+        TileRegs<DP> R;
+        if (t + 1 < T) tile_issue<DP>(a, idx, (t + 1) * RT, vtl, R);
+        if (t >= 1 && jok) {
+          const float* xnr = S.xn[(t - 1) % 3];
+          const int rb = (t - 1) * RT + rh * 16;
+          float cl[16];  // branch-free: clamped rows, value unused when c == 0 or past m
 #pragma unroll
-        for (int i = 0; i < CMAX / NW; ++i) {
-          const int j = wave + NW * i;
-          if (j < ncols) {
-            const int p = S.colprob[j], t = S.coltr[j];
-            const float dist = fmaxf(xnr + Ds[lane * DSD + j], 0.f);
-            const int cs = S.cs[p];
-            const float dmin = (c == 0) ? dist : fminf(dbuf[(static_cast<size_t>(p) * T1 + cs) * m + r], dist);
-            const int slot = (t < cs) ? t : t + 1;
-            dbuf[(static_cast<size_t>(p) * T1 + slot) * m + r] = dmin;
-            pacc[i] += static_cast<double>(dmin);
+          for (int q = 0; q < 16; ++q) cl[q] = closest[min(rb + q, m - 1)];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int rr = rh * 16 + q;
+            if (rb + q < m) {
+              const float dist = fmaxf(xnr[rr] + Ds[rr * DSD + j], 0.f);
+              const float dmin = (c == 0) ? dist : fminf(cl[q], dist);
+              dout[rb + q] = dmin;
+              pacc += static_cast<double>(dmin);
+            }
           }
         }
+        if (t + 1 < T) tile_commit<DP>(Xr + ((t + 1) % 3) * LY::XBUF, S.xn[(t + 1) % 3], vtl, R);
+        __syncthreads();
+        __syncthreads();
       }
-      __syncthreads();
+      if (jok) (rh ? S.potc2 : S.potc)[j] = pacc;
     }
-#pragma unroll
-    for (int i = 0; i < CMAX / NW; ++i) {
-      const int j = wave + NW * i;
-      if (j < ncols) {
-        const double v = wave_sum(pacc[i]);
-        if (lane == 0) S.potc[j] = v;
-      }
-    }
+    __syncthreads();
+    if (tid < ncols) S.potc[tid] += S.potc2[tid];
     __syncthreads();
     if (tid < P && S.K[tid] > c) {
       const int p = tid, j0 = S.colbase[p];
@@ -506,28 +608,28 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     int o = 0;
     for (int p = 0; p < P; ++p) {
       S.off[p] = o;
-      for (int c = 0; c < S.K[p]; ++c) S.colprob[o + c] = static_cast<short>(p);
+      for (int c = 0; c < S.K[p]; ++c) {
+        S.colprob[o + c] = static_cast<short>(p);
+        S.colrow[o + c] = idx[cpos[p * a.Kws + c]];
+      }
       o += S.K[p];
       S.st[p] = ST_RUN;
       S.iter[p] = 0;
     }
     S.ncols = o;
   }
+  for (size_t e = tid; e < static_cast<size_t>(P) * m; e += NT) glab[e] = 0xFF;
   __syncthreads();
   const int ncols = S.ncols;
+  // initial centres (the seeded rows) -> Sm, their norms
   for (int e = tid; e < CMAX * (DP / 4); e += NT) {
     const int col = e / (DP / 4), c4 = e - col * (DP / 4);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (col < ncols) {
-      const int p = S.colprob[col];
-      const int row = idx[cpos[p * a.Kws + (col - S.off[p])]];
-      v = *reinterpret_cast<const float4*>(a.X + static_cast<size_t>(row) * a.ldx + 4 * c4);
-    }
-    *reinterpret_cast<float4*>(Cs + col * DS + 4 * c4) = v;
+    if (col < ncols) v = *reinterpret_cast<const float4*>(a.X + static_cast<size_t>(S.colrow[col]) * a.ldx + 4 * c4);
+    *reinterpret_cast<float4*>(Sm + col * DP + 4 * c4) = v;
   }
-  for (size_t e = tid; e < static_cast<size_t>(P) * m; e += NT) glab[e] = 0xFF;
-  __syncthreads();
-  if (tid < CMAX) S.cnorm[tid] = (tid < ncols) ? row_sq<DP>(Cs + tid * DS, a.dreal) : 0.f;
+  if (tid < CMAX) S.cnorm[tid] = (tid < ncols) ? row_sq(a.X + static_cast<size_t>(S.colrow[tid]) * a.ldx, a.dreal) : 0.f;
+  if (tid < PMAX) S.changed[tid] = 0;
   __syncthreads();
 
   for (;;) {
@@ -539,7 +641,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         const int st = S.st[p];
         if (st == ST_RUN || st == ST_FINAL) {
           any = 1;
-          for (int ct = S.off[p] / 32; ct <= (S.off[p] + S.K[p] - 1) / 32; ++ct) msk |= 1u << ct;
+          for (int q = S.off[p] / 32; q <= (S.off[p] + S.K[p] - 1) / 32; ++q) msk |= 1u << q;
           work += static_cast<unsigned long long>(S.K[p]) * m;
           if (st == ST_RUN) mrows += m;
         }
@@ -549,114 +651,204 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       S.n_lloyd += work;
       S.n_mrows += mrows;
     }
-    if (tid < CMAX) S.cnt[tid] = 0;
-    if (tid < PMAX) S.changed[tid] = 0;
     __syncthreads();
     if (!S.any) break;
-    const unsigned mask = static_cast<unsigned>(S.colmask);
 
-    v16f sacc[2];
-    sacc[0] = v16f{};
-    sacc[1] = v16f{};
-    double iacc[PMAX / NW];
+    // Role-split sweep: both sides execute 2 + 2*(T+1) barriers.
+    if (mrole) {
+      float4 cf[DP / 8];  // register-resident centres of column tile ct
+      const bool active = (S.colmask >> ct) & 1;
+      const int col = ct * 32 + (lane & 31);
+      frag_load<DP>(cf, Sm + col * DP, true, lane);
+      __syncthreads();  // B0: fragments read, Sm may be cleared
+      __syncthreads();  // B1: tile 0 in the ring
+#ifdef CC_KM_STAMPS
+      unsigned long long st_acc[4] = {0, 0, 0, 0};
+#endif
+      for (int t = 0; t <= T; ++t) {
+        KM_STAMP(s0);
+        v16f acc = {};
+        if (active && t < T) mfma_dims<DP, 0, DP / 16>(cf, Xr + (t % 3) * LY::XBUF, acc, lane);
+        KM_STAMP(s1);
+        __syncthreads();
+        KM_STAMP(s2);
+        if (active && t < T) {
+          mfma_dims<DP, DP / 16, DP / 8>(cf, Xr + (t % 3) * LY::XBUF, acc, lane);
+          store_dist(acc, S, Ds, ct, lane);
+        }
+        KM_STAMP(s3);
+        __syncthreads();
+        KM_STAMP(s4);
+        KM_ACC(0, s0, s1);
+        KM_ACC(1, s1, s2);
+        KM_ACC(2, s2, s3);
+        KM_ACC(3, s3, s4);
+      }
+#ifdef CC_KM_STAMPS
+      if (blockIdx.x == 0 && lane == 0 && a.stats)
+        for (int k = 0; k < 4; ++k) atomicAdd(&a.stats[4 + 4 * wave + k], st_acc[k]);
+#endif
+      // old centres -> Co
+      float* co = Co + col * DP + 4 * (lane >> 5);
 #pragma unroll
-    for (int i = 0; i < PMAX / NW; ++i) iacc[i] = 0.0;
-
-    for (int r0 = 0; r0 < m; r0 += RT) {
-      load_tile<DP>(a, idx, r0, Xs, S, tid);
-      __syncthreads();
-      dist_phase<DP>(Cs, Xs, S, Ds, mask, wave, lane);
-      __syncthreads();
-      // E-step: wave per problem, lane per row
+      for (int s = 0; s < DP / 8; ++s) *reinterpret_cast<float4*>(co + 8 * s) = cf[s];
+    } else {
+      __syncthreads();  // B0
       {
-        const int r = r0 + lane;
-        const bool ok = r < m;
+        TileRegs<DP> R;
+        tile_issue<DP>(a, idx, 0, vt, R);
+        tile_commit<DP>(Xr, S.xn[0], vt, R);
+      }
+      __syncthreads();  // B1
+      constexpr int NS = PMAX / NW;  // E-step slots per thread: problems ps + 8i
+      double iacc[NS];
+      unsigned chmask = 0;  // bit i: a label of problem ps + 8i changed in this sweep
+      const int row0 = vt & 31, ps = vt >> 5;
+      int sK[NS], soff[NS], sst[NS];
 #pragma unroll
-        for (int i = 0; i < PMAX / NW; ++i) {
-          const int p = wave + NW * i;
-          if (p >= P) break;
-          const int st = S.st[p];
-          if (st != ST_RUN && st != ST_FINAL) continue;
-          const int K = S.K[p], off = S.off[p];
-          const float* drow = Ds + lane * DSD + off;
-          float best = drow[0];
-          int lab = 0;
-          for (int c = 1; c < K; ++c) {
-            const float v = drow[c];
-            if (v < best) {
-              best = v;
-              lab = c;
+      for (int i = 0; i < NS; ++i) {
+        iacc[i] = 0.0;
+        const int p = ps + NW * i;
+        sst[i] = (p < P) ? S.st[p] : ST_IDLE;
+        sK[i] = (p < P) ? S.K[p] : 0;
+        soff[i] = (p < P) ? S.off[p] : 0;
+      }
+      // M-step role: this wave owns centroid column tile mct, all dims (NDT tiles), counts
+      constexpr int NDT = DP / 32;
+      const int mct = wave - 4;
+      const int mcol = mct * 32 + (lane & 31);
+      int mcl = -1, mpc = 0;
+      if (mcol < ncols) {
+        mpc = S.colprob[mcol];
+        if (S.st[mpc] == ST_RUN) mcl = mcol - S.off[mpc];
+      }
+      const bool mact = __ballot(mcl >= 0) != 0ull;  // wave-uniform: any running column
+      v16f sacc[NDT], cacc = {};
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) sacc[dt] = v16f{};
+      const u32x4 ones = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+#ifdef CC_KM_STAMPS
+      unsigned long long st_acc[4] = {0, 0, 0, 0};
+#endif
+      for (int t = 0; t <= T; ++t) {
+        KM_STAMP(s0);
+        // Opaque copies: keep the compiler from hoisting (and spilling) every per-slot and
+        // per-element address out of the tile loop; they are cheap to recompute.
+        int row = row0, vtl = vt;
+        asm volatile("" : "+v"(row), "+v"(vtl));
+        // phase 1: gather tile t+1 | E-step of tile t-1
+        TileRegs<DP> R;
+        if (t + 1 < T) tile_issue<DP>(a, idx, (t + 1) * RT, vtl, R);
+        if (t >= 1) {
+          const int r = (t - 1) * RT + row;
+          const bool ok = r < m;
+          const float xnr = S.xn[(t - 1) % 3][row];
+          uint8_t old[NS];
+#pragma unroll
+          for (int i = 0; i < NS; ++i)
+            old[i] = (ok && sst[i] == ST_RUN) ? glab[static_cast<size_t>(ps + NW * i) * m + r] : 0;
+#pragma unroll
+          for (int i = 0; i < NS; ++i) {
+            if (sst[i] != ST_RUN && sst[i] != ST_FINAL) continue;
+            const int p = ps + NW * i;
+            const float* drow = Ds + row * DSD + soff[i];
+            const int K = sK[i];
+            float best = drow[0];
+            int lab = 0;
+            for (int c0 = 1; c0 < K; c0 += 8) {  // 8 loads in flight, then strict-< scan
+              float v[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = drow[min(c0 + j, K - 1)];
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                if (c0 + j < K && v[j] < best) {
+                  best = v[j];
+                  lab = c0 + j;
+                }
             }
-          }
-          bool ch = false;
-          if (ok) {
-            uint8_t* gl = glab + static_cast<size_t>(p) * m + r;
-            ch = (*gl != static_cast<uint8_t>(lab));
-            *gl = static_cast<uint8_t>(lab);
-            iacc[i] += static_cast<double>(S.xn[lane]) + static_cast<double>(best);
-          }
-          Ls[p * RT + lane] = ok ? static_cast<uint8_t>(lab) : 0xFF;
-          if (st == ST_RUN) {
-            if (__ballot(ch) != 0ull && lane == 0) S.changed[p] = 1;
-            for (int c = 0; c < K; ++c) {
-              const unsigned long long b = __ballot(ok && lab == c);
-              if (lane == 0) S.cnt[off + c] += static_cast<unsigned>(__popcll(b));
+            if (ok) {
+              if (sst[i] == ST_RUN && old[i] != static_cast<uint8_t>(lab)) chmask |= 1u << i;
+              glab[static_cast<size_t>(p) * m + r] = static_cast<uint8_t>(lab);
+              iacc[i] += static_cast<double>(xnr) + static_cast<double>(best);
             }
+            Ls[p * RT + row] = ok ? static_cast<uint8_t>(lab) : 0xFF;
           }
         }
-      }
-      __syncthreads();
-      // M-step sums: S[col][dim] += sum_row onehot[col][row] * X[row][dim]
+        if (t + 1 < T) tile_commit<DP>(Xr + ((t + 1) % 3) * LY::XBUF, S.xn[(t + 1) % 3], vtl, R);
+        KM_STAMP(s1);
+        __syncthreads();
+        KM_STAMP(s2);
+        // phase 2: M-step of tile t-1 on bf16 MFMA (one-hot A, bf16x3 rows B, ones for counts)
+        if (t >= 1 && mact) {
+          const float* Xb = Xr + ((t - 1) % 3) * LY::XBUF + (lane & 31);
+          const int g8 = 8 * (lane >> 5);
+          constexpr int NQ = (RT / 16) * NDT;  // (k-step, dim tile) pairs
+          float xc[8], xn8[8];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int tau = wave + NW * i;
-        if (tau >= 4 * NDT) break;
-        const int ct = tau / NDT, dt = tau - (tau / NDT) * NDT;
-        if (!((mask >> ct) & 1u)) continue;
-        const int col = ct * 32 + (lane & 31);
-        int pc = -1, cl = -1;
-        if (col < ncols) {
-          pc = S.colprob[col];
-          cl = col - S.off[pc];
-          if (S.st[pc] != ST_RUN) cl = -1;
-        }
-        const uint32_t* lrow = reinterpret_cast<const uint32_t*>(Ls + (pc < 0 ? 0 : pc) * RT);
-        const float* xb = Xs + dt * 32 + (lane & 31);
-        const int g4 = 4 * (lane >> 5);
+          for (int j = 0; j < 8; ++j) xc[j] = Xb[(g8 + j) * LY::XS];
+          u32x4 afr;
 #pragma unroll
-        for (int s = 0; s < RT / 8; ++s) {
-          const uint32_t l4 = lrow[(8 * s + g4) >> 2];
+          for (int q = 0; q < NQ; ++q) {
+            const int ks = q / NDT, dt = q - (q / NDT) * NDT;
+            if (q + 1 < NQ) {  // prefetch the next (k-step, dim tile) rows
+              const int ks1 = (q + 1) / NDT, dt1 = (q + 1) - ((q + 1) / NDT) * NDT;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int lb = static_cast<int>((l4 >> (8 * q)) & 0xFFu);
-            const float av = (lb == cl) ? 1.0f : 0.0f;
-            const float bv = xb[(8 * s + g4 + q) * DS];
-            sacc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, sacc[i], 0, 0, 0);
+              for (int j = 0; j < 8; ++j) xn8[j] = Xb[(16 * ks1 + g8 + j) * LY::XS + dt1 * 32];
+            }
+            if (dt == 0) {  // one-hot of this lane's column over its 8 rows of k-step ks
+              const unsigned long long lab8 =
+                  *reinterpret_cast<const unsigned long long*>(Ls + mpc * RT + 16 * ks + g8);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
+                const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
+                afr[j] = ((b0 == mcl) ? 0x3F80u : 0u) | ((b1 == mcl) ? 0x3F800000u : 0u);
+              }
+              cacc = mfma_bf16(afr, ones, cacc);
+            }
+            u32x4 f0, f1, f2;
+            split3(xc, f0, f1, f2);
+            sacc[dt] = mfma_bf16(afr, f0, sacc[dt]);
+            sacc[dt] = mfma_bf16(afr, f1, sacc[dt]);
+            sacc[dt] = mfma_bf16(afr, f2, sacc[dt]);
+            __builtin_amdgcn_sched_barrier(0);  // bound the live split fragments
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xc[j] = xn8[j];
           }
         }
+        KM_STAMP(s3);
+        __syncthreads();
+        KM_STAMP(s4);
+        KM_ACC(0, s0, s1);
+        KM_ACC(1, s1, s2);
+        KM_ACC(2, s2, s3);
+        KM_ACC(3, s3, s4);
       }
-      __syncthreads();
-    }
-
-    // ---- end of sweep: inertia, sums -> Sn --------------------------------
+#ifdef CC_KM_STAMPS
+      if (blockIdx.x == 0 && (vt & 63) == 0 && a.stats)
+        for (int k = 0; k < 4; ++k) atomicAdd(&a.stats[4 + 4 * wave + k], st_acc[k]);
+#endif
 #pragma unroll
-    for (int i = 0; i < PMAX / NW; ++i) {
-      const int p = wave + NW * i;
-      if (p < P) {
-        const double v = wave_sum(iacc[i]);
-        if (lane == 0) S.sweep_inert[p] = v;
+      for (int i = 0; i < PMAX / NW; ++i) {
+        const int p = ps + NW * i;
+        if (p < P) {
+          const double v = half_sum(iacc[i]);
+          if (row0 == 0) S.sweep_inert[p] = v;
+          if ((chmask >> i) & 1u) S.changed[p] = 1;
+        }
       }
-    }
+      // sums -> Sm (aliases the ring: every ring reader passed the last barrier) ; counts
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int tau = wave + NW * i;
-      if (tau >= 4 * NDT) break;
-      const int ct = tau / NDT, dt = tau - (tau / NDT) * NDT;
+      for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int col = ct * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-        Sn[col * DS + dt * 32 + (lane & 31)] = sacc[i][v];
-      }
+        for (int v = 0; v < 16; ++v) {
+          const int c = mct * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+          Sm[c * DP + dt * 32 + (lane & 31)] = sacc[dt][v];
+        }
+      if ((lane & 31) == 0)
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          S.cnt[mct * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5)] = static_cast<unsigned>(cacc[v]);
     }
     if (tid == 0) {
       int f = 0;
@@ -672,8 +864,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     if (S.flag) {
       for (int p = 0; p < P; ++p) {
         if (S.nempty[p] == 0) continue;
-        relocate<DP>(a, idx, p, Cs, Sn, S, glab,
-                     dbuf + static_cast<size_t>(p) * T1 * m, tid);
+        relocate<DP>(a, idx, p, Co, Sm, S, glab, dbuf + static_cast<size_t>(p) * T1 * m, tid);
         __syncthreads();
       }
     }
@@ -692,17 +883,17 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       const int col = e / DP, d = e - col * DP;
       const int p = S.colprob[col];
       if (S.st[p] != ST_RUN || S.cnt[col] != 0 || col - S.off[p] > S.amax[p]) continue;
-      Sn[col * DS + d] = Sn[(S.off[p] + S.amax[p]) * DS + d];
+      Sm[col * DP + d] = Sm[(S.off[p] + S.amax[p]) * DP + d];
     }
     __syncthreads();
     for (int e = tid; e < ncols * DP; e += NT) {
-      const int col = e / DP, d = e - col * DP;
+      const int col = e / DP;
       const int p = S.colprob[col];
       if (S.st[p] != ST_RUN) continue;
       const unsigned cn = S.cnt[col];
       if (cn > 0) {
         const float alpha = static_cast<float>(1.0 / static_cast<double>(static_cast<float>(cn)));
-        Sn[col * DS + d] *= alpha;
+        Sm[e] *= alpha;
       }
     }
     __syncthreads();
@@ -710,13 +901,13 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       const int col = e / DP, d = e - col * DP;
       const int p = S.colprob[col];
       if (S.st[p] != ST_RUN || S.cnt[col] != 0 || col - S.off[p] < S.amax[p]) continue;
-      Sn[col * DS + d] = Sn[(S.off[p] + S.amax[p]) * DS + d];
+      Sm[col * DP + d] = Sm[(S.off[p] + S.amax[p]) * DP + d];
     }
     __syncthreads();
     // centre shifts (sklearn _euclidean_dense_dense, 4-way unrolled f32)
     if (tid < ncols && S.st[S.colprob[tid]] == ST_RUN) {
-      const float* cn = Sn + tid * DS;
-      const float* co = Cs + tid * DS;
+      const float* cn = Sm + tid * DP;
+      const float* co = Co + tid * DP;
       float res = 0.f;
       const int n4 = a.dreal / 4, rem = a.dreal % 4;
       for (int i = 0; i < n4; ++i) {
@@ -749,20 +940,13 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         S.st[p] = ST_DONE;
         S.inert[p] = static_cast<float>(S.sweep_inert[p]);
       }
+      S.changed[p] = 0;
     }
     __syncthreads();
-    // commit the new centres of problems that sweep again
-    for (int e = tid; e < ncols * (DP / 4); e += NT) {
-      const int col = e / (DP / 4), c4 = e - col * (DP / 4);
-      const int st = S.st[S.colprob[col]];
-      if (st == ST_RUN || st == ST_FINAL)
-        *reinterpret_cast<float4*>(Cs + col * DS + 4 * c4) =
-            *reinterpret_cast<const float4*>(Sn + col * DS + 4 * c4);
-    }
-    __syncthreads();
+    // norms of the centres of problems that sweep again (Sm keeps them for the fragments)
     if (tid < ncols) {
       const int st = S.st[S.colprob[tid]];
-      if (st == ST_RUN || st == ST_FINAL) S.cnorm[tid] = row_sq<DP>(Cs + tid * DS, a.dreal);
+      if (st == ST_RUN || st == ST_FINAL) S.cnorm[tid] = row_sq(Sm + tid * DP, a.dreal);
     }
     __syncthreads();
   }
@@ -845,7 +1029,7 @@ extern "C" int cc_kmeans_plan(const int32_t* Ks, int nK, int n_init, int32_t* gr
   std::vector<int> order(nK);
   for (int i = 0; i < nK; ++i) {
     if (Ks[i] < 1 || Ks[i] > KMAX || Ks[i] * n_init > CMAX || n_init > PMAX) {
-      cc::set_error("cc_kmeans_plan: need 1 <= K <= 127 and K * n_init <= 128 (n_init <= 64)");
+      cc::set_error("cc_kmeans_plan: need 1 <= K <= 127 and K * n_init <= 128 (n_init <= 32)");
       return CC_ERR_UNSUPPORTED;
     }
     order[i] = i;

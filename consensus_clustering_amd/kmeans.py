@@ -19,7 +19,7 @@ import torch
 
 from . import _lib, engine
 
-GSTRIDE = 1 + 4 * 64
+GSTRIDE = 1 + 4 * 32
 DPADS = (32, 64, 128)
 
 
@@ -109,7 +109,7 @@ class BatchedKMeans:
         per_h = lib.cc_kmeans_workspace_bytes(m, g_h.ctypes.data, nG, 1)
         hb = max(1, min(h_end - h_begin, self.workspace_budget // max(per_h, 1)))
         ws = torch.empty(per_h * hb, dtype=torch.uint8, device=dev)
-        self.stats = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.stats = torch.zeros(64, dtype=torch.int64, device=dev)  # [0:4] counters, rest: diagnostics
         ldl = labels_nh.stride(1)
         for h0 in range(h_begin, h_end, hb):
             h1 = min(h_end, h0 + hb)

@@ -98,7 +98,7 @@ int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stre
  * each row once per sweep for all of the group's centroids (<= CC_KM_CMAX columns).
  * Group descriptor g (int32, CC_KM_GSTRIDE entries): [0] = P, then per problem p:
  * [1+4p] = K, [2+4p] = kidx (index into Ks), [3+4p] = init, [4+4p] = local trials. */
-#define CC_KM_PMAX 64
+#define CC_KM_PMAX 32
 #define CC_KM_CMAX 128
 #define CC_KM_GSTRIDE (1 + 4 * CC_KM_PMAX)
 

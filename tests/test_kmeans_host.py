@@ -33,7 +33,7 @@ def test_plan_covers_every_problem_once():
     seen = []
     for row in g:
         P = row[0]
-        assert P % 3 == 0 and P <= 64
+        assert P % 3 == 0 and P <= 32
         cols = 0
         for p in range(P):
             K, kidx, init, ntr = row[1 + 4 * p: 5 + 4 * p]
