@@ -30,11 +30,13 @@ SIGNATURES = {
     "cc_coassoc": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp,
                             _vp, _vp]),
     "cc_consensus": (_c_int, [_vp, _vp, _c_int, _vp, _vp]),
-    "cc_kmeans_plan": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int]),
-    "cc_kmeans_workspace_bytes": (_c_sz, [_c_int, _vp, _c_int, _c_int]),
-    "cc_kmeans_batched": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int,
-                                   _c_int, _vp, _vp, _c_int, _c_int, _c_int, _c_dbl, _vp, _c_int,
-                                   _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "cc_kmeans_plan": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int]),
+    "cc_kmeans_workspace_bytes": (_c_sz, [_c_int, _c_int, _vp, _c_int, _c_int, _c_int]),
+    "cc_split_f16": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
+    "cc_kmeans_batched": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
+                                   _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_int, _c_int,
+                                   _c_dbl, _vp, _c_int, _vp, _vp, _c_int, _vp, _vp, _vp, _vp,
+                                   _c_sz, _c_int, _c_int, _vp]),
 }
 
 _lock = threading.Lock()

@@ -161,14 +161,15 @@ class ConsensusClustering:
         km = self._kmeans_params()
         self.backend_ = 'gpu-kmeans' if km is not None else 'host-clusterer'
         if Ks and km is not None:
-            Xd, xnorm, _ = _prepare(X, dev)
+            Xd, xnorm, _, Xhl, sexp = _prepare(X, dev)
             bk = BatchedKMeans(Ks, n_init=km["n_init"], max_iter=km["max_iter"], tol=km["tol"],
                                random_state=self.random_state,
                                workspace_budget=self.workspace_budget)
             self.kmeans_inertia_ = torch.zeros((len(Ks), H), dtype=torch.float32, device=dev)
             self.kmeans_n_iter_ = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
             bk.run(Xd, xnorm, X.shape[1], idx_d, n, H, m, h0, h1, labels, weight_dtype=wdtype,
-                   inertia=self.kmeans_inertia_, n_iter=self.kmeans_n_iter_)
+                   inertia=self.kmeans_inertia_, n_iter=self.kmeans_n_iter_, Xhl=Xhl,
+                   scale_exp=sexp)
             self.kmeans_stats_ = bk.stats
         elif Ks:
             if isinstance(X, torch.Tensor):

@@ -1,37 +1,46 @@
-// Batched k-means for every (resample, K, init) problem of a consensus fit, on gfx950.
+// Batched k-means for every (resample, K, init) problem of a consensus fit, on gfx950 (v3).
 //
 // Replaces the per-(K, h) `clusterer.fit_predict(X[indices])` of the reference
 // (consensus_clustering_parallelised.py:282, default clusterer KMeans(), CC.py:88-90,
-// with set_params(random_state=seed, n_init=3), CC.py:212-214) by launches that run
-// every problem at once.  The algorithm is scikit-learn's KMeans (sklearn/cluster/_kmeans.py):
-//   * k-means++ seeding (:174-262): first centre from RandomState(seed).choice with
-//     uniform p (resolved on the host), then per centre 2+floor(ln K) candidates drawn
-//     by searchsorted(cumsum(closest d^2), u * pot), the candidate minimising the
-//     potential kept;  every fit of one K replays the same RandomState(seed) stream;
-//   * Lloyd (:624-752, _k_means_lloyd.pyx:23-212): labels = argmin_c |c|^2 - 2 x.c
-//     (strict <, lowest index on ties), centres = sums * f32(1/count), empty clusters
-//     relocated to the farthest points (_k_means_common.pyx:167-212), strict
-//     convergence on unchanged labels else sum(shift^2) <= tol, tol = 1e-4 * mean var,
-//     a final E-step when not strictly converged;
+// with set_params(random_state=seed, n_init=3), CC.py:212-214).  The algorithm is
+// scikit-learn's KMeans (sklearn/cluster/_kmeans.py):
+//   * k-means++ seeding (:174-262): first centre from RandomState(seed).choice (resolved on
+//     the host), then per centre 2+floor(ln K) candidates drawn by
+//     searchsorted(cumsum(closest d^2), u * pot), the candidate minimising the potential
+//     kept; every fit of one K replays the same RandomState(seed) stream;
+//   * Lloyd (:624-752, _k_means_lloyd.pyx:23-212): labels = argmin_c |c|^2 - 2 x.c (strict
+//     <, lowest index on ties), centres = sums * f32(1/count), empty clusters relocated to
+//     the farthest points (_k_means_common.pyx:167-212), strict convergence on unchanged
+//     labels else sum(shift^2) <= tol, tol = 1e-4 * mean var, a final E-step when not
+//     strictly converged;
 //   * best of n_init: lower inertia AND a different clustering (:1525-1531).
 //
-// Mapping.  A workgroup (512 threads, ~145 KiB LDS, one per CU) owns one resample h and
-// one GROUP of problems (<= 128 centroid columns, <= 32 problems; all n_init runs of a
-// K in one group) and runs their whole fits on-chip.  The resample's rows stream
-// through LDS in 32-row tiles, once per sweep for ALL the group's centroids.  The 8
-// waves are specialised, one of each kind per SIMD:
-//   MFMA waves (0-3)  wave w owns centroid columns 32w..32w+31 as register-resident
-//                     A fragments and computes D = |c|^2 - 2 c.x for the tile on
-//                     v_mfma_f32_32x32x2_f32 (exact f32 fma chain);
-//   VALU waves (4-7)  gather the next tile's rows into LDS, run the E-step of the
-//                     previous tile (argmin per row and problem: strict <, lowest
-//                     index) and its M-step (per-(column, dim) owner threads add the
-//                     rows into LDS sums with ds_add_f32: one owner per address, rows
-//                     in order -> deterministic sums).
-// The two kinds overlap through a 3-deep tile ring with two workgroup barriers per
-// tile: tile t's distances (MFMA) run beside tile t-1's E/M-steps and tile t+1's gather.
-// Nothing crosses workgroups, so results do not depend on scheduling or on how the
-// resamples are sharded over launches or GPUs.
+// Mapping (v3).  A persistent grid (one 512-thread workgroup per CU, ~150 KiB LDS) pulls
+// UNITS = (resample h, subset of the (K, init) problems) from an atomic counter and runs a
+// unit's whole set of fits on-chip.  A unit is driven as a problem ENGINE: every SWEEP
+// streams the resample's rows once through LDS (32-row tiles) and serves up to 256 centroid
+// "slots": the candidate columns of problems that are seeding (k-means++) and the centres of
+// problems in Lloyd.  Between sweeps the engine retires converged problems, admits new ones
+// and packs the next sweep round-robin, so no slot idles behind a group's slowest init.
+//
+// Arithmetic.  Rows and centres enter the MFMA as f16 hi/lo pairs of x * 2^s (the exact
+// power-of-two scale keeps the pair inside f16 range): x.c = xh.ch + xh.cl + xl.ch, three
+// v_mfma_f32_32x32x16_f16 per 16 dims with f32 accumulation (22 significant bits per
+// operand, the accuracy class of sklearn's own float32 sgemm), 5.3x the f32-MFMA rate.  The
+// M-step sums are a one-hot x (xh + xl) f16 MFMA (exact one-hot products, f32 sums), the
+// counts a one-hot x ones MFMA.  All decisions (argmin, potentials, convergence, relocation,
+// best-of-init) are f32/f64 as in sklearn.
+//
+// The 8 waves are uniform.  Wave w owns centroid slots 32w..32w+31 (register-resident f16
+// A fragments) and, per tile iteration t (one barrier each), does
+//   dist MFMA of tile t -> LDS distance tile (double buffer),
+//   E-step of tile t-1 (all 512 threads: thread = (row, work item); argmin per Lloyd
+//     problem, min-with-closest per seeding candidate),
+//   M-step of tile t-2 (one-hot A from the E-step labels, B = the X tile read back with
+//     ds_read_b64_tr_b16 from the same swizzled image the distance reads row-wise),
+//   and the gather of tile t+1 into a 4-slot ring.
+// Nothing crosses workgroups, so results do not depend on scheduling, on how the units are
+// split over launches or over GPUs.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,30 +54,37 @@
 namespace {
 
 typedef float v16f __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef short s4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4 lds_s4;
 
 constexpr int NT = 512;
 constexpr int NW = 8;
-constexpr int NVT = 256;            // VALU-role threads (waves 4..7)
 constexpr int RT = 32;              // rows per tile (one MFMA row block)
-constexpr int CMAX = CC_KM_CMAX;    // 128 centroid / candidate columns (4 MFMA waves x 32)
-constexpr int PMAX = CC_KM_PMAX;    // 64 problems per group
+constexpr int CW = 256;             // centroid slots per sweep (8 waves x 32)
+constexpr int NS = 8;               // E-step work items per thread (16 item lanes x 8)
+constexpr int IMAX = 16 * NS;       // work items per sweep
+constexpr int PMAX = CC_KM_PMAX;    // problems per unit
 constexpr int TMAX = 6;             // max local trials: 2 + floor(ln 127)
-constexpr int DSD = CMAX + 1;       // distance-tile row stride (floats)
-constexpr int GS = CC_KM_GSTRIDE;
 constexpr int KMAX = 127;
+constexpr int DSD = CW + 1;         // distance-tile row stride (floats): conflict-free b32 reads
+constexpr int NRING = 4;            // X tile ring: t+1 (gather), t (dist), t-2 (M-step)
+constexpr int US = CC_KM_USTRIDE;
 
-enum { ST_IDLE = 0, ST_RUN = 1, ST_FINAL = 2, ST_DONE = 3 };
+enum { ST_WAIT = 0, ST_SEED = 1, ST_RUN = 2, ST_FINAL = 3, ST_DONE = 4 };
+enum { IK_SEED0 = 0, IK_SEED = 1, IK_RUN = 2, IK_FINAL = 3 };
 
 struct KArgs {
-  const float* X;
-  const float* xnorm;
-  int ldx, dreal;
+  const float* X;          // [n][DP] f32 (mean-centred, zero-padded)
+  const uint16_t* Xhl;     // [n][2][DP] f16 bits: hi, lo of X * 2^s
+  const float* xnorm;      // [n]
+  int dreal;
+  float scale, inv_scale, dscale;  // 2^s, 2^-s, 2^(1-2s)
   const int32_t* idx;
-  int m, h_begin, nh;
-  const int32_t* groups;
-  int nG;
+  int m, h_begin, nh, T;
+  const int32_t* units;
+  int nU;
   int max_iter;
   double tol_rel;
   const double* kpp_u;
@@ -79,51 +95,68 @@ struct KArgs {
   float* inertia_out;
   int32_t* niter_out;
   unsigned long long* stats;
+  unsigned* counter;
   uint8_t* ws;
-  size_t ws_per_wg, off_dbuf, off_cpos;
-  int Pws, Tws, Kws;
+  size_t ws_per_wg, off_cen, off_cenn, off_cpos, off_dbuf, off_tsum, off_rdist;
+  int Pws, Kws, Tws, seedmax;
 };
 
-// Small per-workgroup state (LDS).
 struct State {
-  int K[PMAX], kidx[PMAX], init[PMAX], ntr[PMAX], off[PMAX], st[PMAX], iter[PMAX], cs[PMAX];
-  int colbase[PMAX], amax[PMAX], nempty[PMAX];
-  unsigned changed[PMAX];
+  // unit
+  int unit, P;
+  float tol;
+  int rr;
+  unsigned seedfree;
+  // problems
+  unsigned char K[PMAX], kidx[PMAX], init[PMAX], ntr[PMAX], st[PMAX], c[PMAX], cs[PMAX], sslot[PMAX];
+  unsigned char need_sel[PMAX], to_run[PMAX], sbest[PMAX];
+  short cenoff[PMAX], pitem[PMAX];
+  int iter[PMAX], amax[PMAX], nempty[PMAX];
   float pot32[PMAX], inert[PMAX];
-  double sweep_inert[PMAX];
   int cand[PMAX][TMAX];
-  short colprob[CMAX], coltr[CMAX];
-  int colrow[CMAX];  // source row of each MFMA column (seeding candidates / initial centres)
-  unsigned cnt[CMAX];
-  float cnorm[CMAX], shift[CMAX];
-  double potc[CMAX], potc2[CMAX];
-  float xn[3][RT];
-  int map[KMAX + 1];
+  // sweep
+  int nitems, ncols;
+  unsigned char ikind[IMAX], iprob[IMAX], itr[IMAX];
+  short ioff[IMAX], incol[IMAX];
+  double iinert[IMAX];
+  unsigned ichanged[IMAX];
+  short sitem[CW], scl[CW];
+  int srow[CW];  // >= 0: X row (seeding candidate); < 0: -(centre row) - 1
+  float cnorm[CW], shift[CW];
+  unsigned cnt[CW];
+  // scratch
   double red_v[NW];
   int red_i[NW];
-  int P, ncols, colmask, any, flag, Kg;
-  float tol;
-  unsigned long long n_lloyd, n_seed, n_mrows, n_reloc;
+  int map[KMAX + 1];
+  int flag;
+  unsigned long long n_lloyd, n_seed, n_mrows, n_reloc, n_sweeps, n_ctiles;
 };
 
 template <int DP>
 struct Lay {
-  static constexpr int XS = DP + 4;            // X tile row stride (floats): conflict-free b128 reads
-  static constexpr int XBUF = RT * XS;         // floats per X ring slot
-  static constexpr int OFF_D = 3 * XBUF * 4;   // distance tile [RT][DSD]
-  static constexpr int U_END = OFF_D + RT * DSD * 4;
-  static constexpr int S_BYTES = CMAX * DP * 4;      // sums / new centres, aliasing the ring
-  static_assert(S_BYTES <= U_END, "centre sums must fit in the tile ring");
-  static constexpr int OFF_CO = (U_END + 15) / 16 * 16;  // old centres [CMAX][DP]
-  static constexpr int OFF_LS = OFF_CO + S_BYTES;        // tile labels [PMAX][RT]
-  static constexpr int OFF_ST = OFF_LS + RT * PMAX;
+  static constexpr int IMG = RT * DP * 2;     // one f16 image (hi or lo) of a tile, bytes
+  static constexpr int SLOT = 2 * IMG;        // ring slot: hi image then lo image
+  static constexpr int OFF_D = NRING * SLOT;  // distance tiles [2][RT][DSD] f32
+  static constexpr int DBUF = RT * DSD * 4;
+  static constexpr int U_END = OFF_D + 2 * DBUF;
+  static constexpr int S_BYTES = CW * DP * 4;  // centre sums [CW][DP] f32, aliasing ring + D
+  static_assert(S_BYTES <= U_END, "centre sums must fit in the ring + distance tiles");
+  static constexpr int OFF_LS = (U_END + 15) / 16 * 16;  // labels [2][IMAX][RT] u8
+  static constexpr int OFF_XN = OFF_LS + 2 * IMAX * RT;  // row norms [NRING][RT] f32
+  static constexpr int OFF_ST = OFF_XN + NRING * RT * 4;
   static constexpr int TOTAL = OFF_ST + ((sizeof(State) + 15) / 16) * 16;
+  static_assert(TOTAL <= 163840, "LDS budget");
 };
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+// Byte offset of 16-B chunk `ch` of tile row `row` in one f16 image (DP/8 chunks per row).
+// XOR-swizzled so that both the row-wise ds_read_b128 of the distance B operand (32 rows,
+// one chunk) and the ds_read_b64_tr_b16 of the M-step B operand (4 rows x 32 dims per
+// 32-lane half) are bank-conflict free (bank = (addr/4) mod 64).
+template <int DP>
+__device__ __forceinline__ int xoff(int row, int ch) {
+  if constexpr (DP == 128) return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+  else if constexpr (DP == 64) return 128 * row + 16 * (ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3)));
+  else return 64 * row + 16 * (ch ^ ((row >> 2) & 3));
 }
 
 __device__ __forceinline__ double half_sum(double v) {  // over the 32 lanes of a half-wave
@@ -132,18 +165,9 @@ __device__ __forceinline__ double half_sum(double v) {  // over the 32 lanes of 
   return v;
 }
 
-// Diagnostic build only (-DCC_KM_STAMPS): per-wave cycle accounting of the Lloyd sweep
-// phases of workgroup 0, added into stats[4 + 4*wave + k] (k: work1, wait1, work2, wait2).
-#ifdef CC_KM_STAMPS
-#define KM_STAMP(var) \
-  __builtin_amdgcn_sched_barrier(0); \
-  const unsigned long long var = __builtin_amdgcn_s_memtime(); \
-  __builtin_amdgcn_sched_barrier(0)
-#define KM_ACC(k, a, b) st_acc[k] += (b) - (a)
-#else
-#define KM_STAMP(var)
-#define KM_ACC(k, a, b)
-#endif
+__device__ __forceinline__ v16f mfma16(const h8& a, const h8& b, const v16f& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 
 // numpy pairwise_sum of a short contiguous float32 array (n <= 128), as
 // `(center_shift ** 2).sum()` evaluates it (numpy/_core/src/umath/loops_utils.h).
@@ -172,127 +196,89 @@ __device__ __forceinline__ float row_sq(const float* c, int dreal) {
   return s;
 }
 
-// ---- VALU-role tile gather: issue the global loads early, commit to LDS late ----
+// ---- X tile gather (all threads): issue the global loads early, commit to LDS late ----
 template <int DP>
 struct TileRegs {
-  static constexpr int PER = RT * (DP / 4) / NVT;  // float4 per VALU thread (1, 2 or 4)
-  float4 v[PER];
+  static constexpr int CPR = DP / 4;            // 16-B chunks per row (hi + lo)
+  static constexpr int NCH = RT * CPR;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  u32x4 v[PER];
   float xn;
 };
 
 template <int DP>
-__device__ __forceinline__ void tile_issue(const KArgs& a, const int32_t* idx, int r0, int vt,
+__device__ __forceinline__ void tile_issue(const KArgs& a, const int32_t* idx, int r0, int tid,
                                            TileRegs<DP>& R) {
-  // Branch-free gather: all row indices first, then all rows (two dependent round trips).
-  constexpr int NV = DP / 4;
-  constexpr int PER = TileRegs<DP>::PER;
-  int src[PER];
+  using TR = TileRegs<DP>;
+  int src[TR::PER];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int row = (vt + NVT * i) / NV;
-    src[i] = idx[min(r0 + row, a.m - 1)];
+  for (int i = 0; i < TR::PER; ++i) {
+    const int e = tid + NT * i;
+    src[i] = idx[min(r0 + min(e / TR::CPR, RT - 1), a.m - 1)];
   }
-  const int xr = min(r0 + (vt & (RT - 1)), a.m - 1);
+  const int xr = min(r0 + (tid & (RT - 1)), a.m - 1);
   const float xn = a.xnorm[idx[xr]];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int e = vt + NVT * i;
-    const int row = e / NV, c4 = e - (e / NV) * NV;
-    const float4 v = *reinterpret_cast<const float4*>(a.X + static_cast<size_t>(src[i]) * a.ldx + 4 * c4);
-    const bool ok = r0 + row < a.m;
-    R.v[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < TR::PER; ++i) {
+    const int e = tid + NT * i;
+    const int row = e / TR::CPR, c = e - (e / TR::CPR) * TR::CPR;
+    const bool ok = e < TR::NCH && r0 + row < a.m;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (e < TR::NCH) v = *reinterpret_cast<const u32x4*>(a.Xhl + static_cast<size_t>(src[i]) * (2 * DP) + 8 * c);
+    R.v[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
   }
-  R.xn = (r0 + (vt & (RT - 1)) < a.m) ? xn : 0.f;
+  R.xn = (r0 + (tid & (RT - 1)) < a.m) ? xn : 0.f;
 }
 
 template <int DP>
-__device__ __forceinline__ void tile_commit(float* Xb, float* xn, int vt, const TileRegs<DP>& R) {
+__device__ __forceinline__ void tile_commit(char* slot, float* xn, int tid, const TileRegs<DP>& R) {
+  using TR = TileRegs<DP>;
   using LY = Lay<DP>;
-  constexpr int NV = DP / 4;
 #pragma unroll
-  for (int i = 0; i < TileRegs<DP>::PER; ++i) {
-    const int e = vt + NVT * i;
-    const int row = e / NV, c4 = e - (e / NV) * NV;
-    *reinterpret_cast<float4*>(Xb + row * LY::XS + 4 * c4) = R.v[i];
+  for (int i = 0; i < TR::PER; ++i) {
+    const int e = tid + NT * i;
+    if (e < TR::NCH) {
+      const int row = e / TR::CPR, c = e - (e / TR::CPR) * TR::CPR;
+      const int part = c / (DP / 8), ch = c - part * (DP / 8);
+      *reinterpret_cast<u32x4*>(slot + part * LY::IMG + xoff<DP>(row, ch)) = R.v[i];
+    }
   }
-  if (vt < RT) xn[vt] = R.xn;
+  if (tid < RT) xn[tid] = R.xn;
 }
 
-// ---- MFMA-role helpers -------------------------------------------------------
-// Fragment of column (32*ct + lane%32): dims 8s + 4*(lane/32) .. +3 for s < DP/8.
+// A fragments of one centroid slot: lane (r, h) holds dims 16s + 8h + j of its slot's centre.
 template <int DP>
-__device__ __forceinline__ void frag_load(float4 (&cf)[DP / 8], const float* src, bool valid, int lane) {
-  const int g4 = 4 * (lane >> 5);
+__device__ __forceinline__ void afrag_load(h8 (&ah)[DP / 16], h8 (&al)[DP / 16], const float* src,
+                                           bool valid, int h, float scale) {
 #pragma unroll
-  for (int s = 0; s < DP / 8; ++s)
-    cf[s] = valid ? *reinterpret_cast<const float4*>(src + 8 * s + g4) : make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-template <int DP, int S0, int S1>
-__device__ __forceinline__ void mfma_dims(const float4 (&cf)[DP / 8], const float* Xb, v16f& acc, int lane) {
-  using LY = Lay<DP>;
-  const float* bp = Xb + (lane & 31) * LY::XS + 4 * (lane >> 5);
+  for (int s = 0; s < DP / 16; ++s) {
+    float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+    if (valid) {
+      x0 = *reinterpret_cast<const float4*>(src + 16 * s + 8 * h);
+      x1 = *reinterpret_cast<const float4*>(src + 16 * s + 8 * h + 4);
+    }
+    const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-  for (int s = S0; s < S1; ++s) {
-    const float4 bv = *reinterpret_cast<const float4*>(bp + 8 * s);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf[s].x, bv.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf[s].y, bv.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf[s].z, bv.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cf[s].w, bv.w, acc, 0, 0, 0);
+    for (int j = 0; j < 8; ++j) {
+      const float xs = x[j] * scale;
+      const _Float16 hi = static_cast<_Float16>(xs);
+      ah[s][j] = hi;
+      al[s][j] = static_cast<_Float16>(xs - static_cast<float>(hi));
+    }
   }
-}
-
-// Ds[row][col] = cnorm[col] - 2 acc  (acc = D[col][row]: lane = row, regs = columns)
-__device__ __forceinline__ void store_dist(const v16f& acc, const State& S, float* Ds, int ct, int lane) {
-  float* drow = Ds + (lane & 31) * DSD + ct * 32 + 4 * (lane >> 5);
-  const float* cn = S.cnorm + ct * 32 + 4 * (lane >> 5);
-#pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const int i = (v & 3) + 8 * (v >> 2);
-    drow[i] = cn[i] - 2.0f * acc[v];
-  }
-}
-
-// ---- M-step on bf16 MFMA: S[col][dim] += sum_rows onehot[col][row] * x[row][dim] ----
-// x = x0 + x1 + x2 with bf16 x0 = RN(x), x1 = RN(x - x0), x2 = RN(x - x0 - x1): the one-hot
-// products are exact and the three bf16 MFMAs add the row's value back to f32 precision.
-__device__ __forceinline__ unsigned bf16_pack(float a, float b) {
-  return static_cast<unsigned>(__builtin_bit_cast(unsigned short, static_cast<__bf16>(a))) |
-         (static_cast<unsigned>(__builtin_bit_cast(unsigned short, static_cast<__bf16>(b))) << 16);
-}
-__device__ __forceinline__ float bf16_lo(unsigned p) { return __builtin_bit_cast(float, p << 16); }
-__device__ __forceinline__ float bf16_hi(unsigned p) { return __builtin_bit_cast(float, p & 0xFFFF0000u); }
-
-// 8 f32 values -> 3 bf16x8 fragments (hi, mid, lo parts)
-__device__ __forceinline__ void split3(const float (&x)[8], u32x4& f0, u32x4& f1, u32x4& f2) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float a = x[2 * i], b = x[2 * i + 1];
-    const unsigned p0 = bf16_pack(a, b);
-    const float ra = a - bf16_lo(p0), rb = b - bf16_hi(p0);
-    const unsigned p1 = bf16_pack(ra, rb);
-    const unsigned p2 = bf16_pack(ra - bf16_lo(p1), rb - bf16_hi(p1));
-    f0[i] = p0;
-    f1[i] = p1;
-    f2[i] = p2;
-  }
-}
-
-__device__ __forceinline__ v16f mfma_bf16(const u32x4& a, const u32x4& b, const v16f& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
-                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
 
 // Empty-cluster relocation for problem p (rare path; _k_means_common.pyx:167-212).
-// Sm holds the un-averaged sums [CMAX][DP], Co the centres the labels came from.
+// Sm holds the un-averaged sums of the problem's slots [off, off+K), cen the centres the
+// labels came from.
 template <int DP>
-__device__ void relocate(const KArgs& a, const int32_t* idx, int p, const float* Co, float* Sm,
-                         State& S, const uint8_t* glab, float* dist, int tid) {
-  const int m = a.m, off = S.off[p], K = S.K[p];
+__device__ void relocate(const KArgs& a, const int32_t* idx, int p, int off, const float* cen,
+                         float* Sm, State& S, const uint8_t* glab, float* dist, int tid) {
+  const int m = a.m, K = S.K[p];
   float mymax = 0.f;
   for (int r = tid; r < m; r += NT) {
-    const float* x = a.X + static_cast<size_t>(idx[r]) * a.ldx;
-    const float* c = Co + (off + glab[static_cast<size_t>(p) * m + r]) * DP;
+    const float* x = a.X + static_cast<size_t>(idx[r]) * DP;
+    const float* c = cen + (S.cenoff[p] + glab[static_cast<size_t>(p) * m + r]) * DP;
     float s = 0.f;
     for (int d = 0; d < a.dreal; ++d) {
       const float t = x[d] - c[d];
@@ -348,7 +334,7 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, const float*
         gi = S.red_i[w];
       }
     const int old = glab[static_cast<size_t>(p) * m + gi];
-    const float* x = a.X + static_cast<size_t>(idx[gi]) * a.ldx;
+    const float* x = a.X + static_cast<size_t>(idx[gi]) * DP;
     for (int d = tid; d < DP; d += NT) {
       Sm[(off + old) * DP + d] -= x[d];
       Sm[(off + c) * DP + d] = x[d];
@@ -364,621 +350,688 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, const float*
   }
 }
 
+// k-means++ candidate positions for centre S.c[p] (>= 1) of problem p, one wave:
+// searchsorted(cumsum(closest), u * pot) (side='left': #{cumsum < v}), clipped to m-1.
+// The cumsum is blocked: f64 prefix over the per-tile sums of the chosen candidate
+// (written by the E-step), then an f64 running sum inside the crossing tile.
+__device__ void kpp_select(const KArgs& a, State& S, int p, const float* closest,
+                           const double* tsum, int lane) {
+  const int ntr = S.ntr[p], c = S.c[p], m = a.m, T = a.T;
+  const double* u = a.kpp_u + (static_cast<size_t>(S.kidx[p]) * a.n_init + S.init[p]) * a.kpp_stride +
+                    1 + static_cast<size_t>(c - 1) * ntr;
+  const double pot = static_cast<double>(S.pot32[p]);
+  double rv[TMAX], base[TMAX];
+  int tau[TMAX];
+  bool found[TMAX];
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) {
+    rv[t] = (t < ntr) ? u[t] * pot : 0.0;
+    base[t] = 0.0;
+    tau[t] = T;
+    found[t] = false;
+  }
+  double run = 0.0;
+  for (int b = 0; b < T; b += 64) {
+    const int j = b + lane;
+    double v = (j < T) ? tsum[j] : 0.0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double y = __shfl_up(v, o);
+      if (lane >= o) v += y;
+    }
+    const double cum = run + v;
+    const int nvalid = min(64, T - b);
+#pragma unroll
+    for (int t = 0; t < TMAX; ++t) {
+      if (t >= ntr) continue;
+      const int k = __popcll(__ballot(j < T && cum < rv[t]));
+      const double prev = __shfl(cum, max(k - 1, 0));
+      if (!found[t] && k < nvalid) {
+        found[t] = true;
+        tau[t] = b + k;
+        base[t] = (k == 0) ? run : prev;
+      }
+    }
+    run = __shfl(cum, 63);
+  }
+  // within the crossing tile: lane t walks its 32 rows
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) {
+    if (t >= ntr || lane != t) continue;
+    int pos = m;
+    if (found[t]) {
+      const int r0 = RT * tau[t];
+      double acc = base[t];
+      int k = 0;
+      for (; k < RT && r0 + k < m; ++k) {
+        acc += static_cast<double>(closest[r0 + k]);
+        if (!(acc < rv[t])) break;
+      }
+      pos = r0 + k;
+    }
+    S.cand[p][t] = min(pos, m - 1);
+  }
+}
+
+// ---- E-step (all 512 threads): thread = (row er = tid & 31, item lane eq = tid >> 5), items
+// eq + 16 i.  Lloyd items: argmin over the problem's K slots (strict <, lowest index), label
+// change, inertia; seeding items: min with the closest distance, potential, tile sums.
+struct EState {
+  double iacc[NS];
+  unsigned chmask;
+};
+
+__device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, int t, int T, int nitems,
+                                               int tidl, const uint8_t* glab, const float* dbuf, int T1,
+                                               unsigned (&pre)[NS]) {
+  const int m = a.m;
+  const int erow = (t - 1) * RT + (tidl & (RT - 1));
+  const bool eok = (t >= 1 && t <= T) && erow < m;
+  const int eql = tidl >> 5;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    pre[i] = 0;
+    const int it = eql + 16 * i;
+    if (eok && it < nitems) {
+      const int kind = S.ikind[it], p = S.iprob[it];
+      if (kind == IK_RUN)
+        pre[i] = glab[static_cast<size_t>(p) * m + erow];
+      else if (kind == IK_SEED)
+        pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(S.sslot[p]) * T1 + S.cs[p]) * m + erow]);
+    }
+  }
+}
+
+template <int DP>
+__device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int T, int nitems, int tidl,
+                                      const float* Dt, uint8_t* Ls, const float* XN, uint8_t* glab,
+                                      float* dbuf, double* tsum, int T1, const unsigned (&pre)[NS],
+                                      EState& es) {
+  if (t < 1 || t > T) return;
+  const int m = a.m;
+  const int te = t - 1;
+  const int ler = tidl & (RT - 1), eql = tidl >> 5;
+  const int erow = te * RT + ler;
+  const bool eok = erow < m;
+  const float* drow = Dt + (te & 1) * (RT * DSD) + ler * DSD;
+  uint8_t* lsb = Ls + (te & 1) * (IMAX * RT);
+  const float xnr = XN[(te % NRING) * RT + ler];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int it = eql + 16 * i;
+    if (it >= nitems) continue;  // uniform per half-wave
+    const int kind = S.ikind[it], p = S.iprob[it], off = S.ioff[it];
+    if (kind >= IK_RUN) {
+      const int K = S.incol[it];
+      const float* dr = drow + off;
+      float best = dr[0];
+      int lab = 0;
+      for (int c0 = 1; c0 < K; c0 += 8) {  // 8 loads in flight, then strict-< scan
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = dr[min(c0 + j, K - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (c0 + j < K && v[j] < best) {
+            best = v[j];
+            lab = c0 + j;
+          }
+      }
+      if (eok) {
+        if (kind == IK_RUN && pre[i] != static_cast<unsigned>(lab)) es.chmask |= 1u << i;
+        glab[static_cast<size_t>(p) * m + erow] = static_cast<uint8_t>(lab);
+        es.iacc[i] += static_cast<double>(xnr) + static_cast<double>(best);
+      }
+      lsb[it * RT + ler] = eok ? static_cast<uint8_t>(lab) : 0xFF;
+    } else {
+      const int tr = S.itr[it], ss = S.sslot[p];
+      const float dist = fmaxf(xnr + drow[off], 0.f);
+      float dm = dist;
+      int slot = 0;
+      if (kind == IK_SEED) {
+        dm = fminf(__uint_as_float(pre[i]), dist);
+        const int cs = S.cs[p];
+        slot = (tr < cs) ? tr : tr + 1;
+      }
+      const double dv = eok ? static_cast<double>(dm) : 0.0;
+      if (eok) dbuf[(static_cast<size_t>(ss) * T1 + slot) * m + erow] = dm;
+      es.iacc[i] += dv;
+      const double ts = half_sum(dv);
+      if (ler == 0) tsum[(static_cast<size_t>(ss) * a.Tws + tr) * T + te] = ts;
+    }
+  }
+}
+
+__device__ __forceinline__ void estep_finish(State& S, int nitems, int tid, const EState& es) {
+  const int er = tid & (RT - 1), eq = tid >> 5, hh = (tid & 63) >> 5;
+#pragma unroll
+  for (int i = 0; i < NS; ++i) {
+    const int it = eq + 16 * i;
+    const double v = half_sum(es.iacc[i]);
+    const unsigned long long bal = __ballot((es.chmask >> i) & 1u);
+    const unsigned halfbits = static_cast<unsigned>(bal >> (32 * hh));
+    if (it < nitems && er == 0) {
+      S.iinert[it] = v;
+      S.ichanged[it] = halfbits != 0u;
+    }
+  }
+}
+
+// Thread 0: admit waiting problems into free seeding slots, then pack the next sweep:
+// seeding candidates first (they are on every problem's critical path), then Lloyd
+// problems round-robin from S.rr, first fit into the CW slots.
+__device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
+  const int P = S.P;
+  for (int p = 0; p < P && S.seedfree; ++p) {
+    if (S.st[p] != ST_WAIT) continue;
+    const int s = __ffs(S.seedfree) - 1;
+    S.seedfree &= ~(1u << s);
+    S.sslot[p] = static_cast<unsigned char>(s);
+    S.st[p] = ST_SEED;
+    S.c[p] = 0;
+  }
+  int ni = 0, nc = 0;
+  unsigned long long nseed = 0, nlloyd = 0, nm = 0;
+  for (int p = 0; p < P; ++p) S.pitem[p] = -1;
+  for (int p = 0; p < P; ++p) {
+    if (S.st[p] != ST_SEED) continue;
+    const int c = S.c[p];
+    const int nt = (c == 0) ? 1 : S.ntr[p];
+    if (nc + nt > CW || ni + nt > IMAX) continue;
+    S.pitem[p] = static_cast<short>(ni);
+    for (int t = 0; t < nt; ++t) {
+      S.ikind[ni] = static_cast<unsigned char>(c == 0 ? IK_SEED0 : IK_SEED);
+      S.iprob[ni] = static_cast<unsigned char>(p);
+      S.ioff[ni] = static_cast<short>(nc);
+      S.incol[ni] = 1;
+      S.itr[ni] = static_cast<unsigned char>(t);
+      const int pos = (c == 0) ? a.kpp_pos[S.kidx[p] * a.n_init + S.init[p]] : S.cand[p][t];
+      S.sitem[nc] = static_cast<short>(ni);
+      S.scl[nc] = -1;
+      S.srow[nc] = idx[pos];
+      ++ni;
+      ++nc;
+    }
+    nseed += static_cast<unsigned long long>(nt) * a.m;
+  }
+  int first_skip = -1, last = -1;
+  for (int j = 0; j < P; ++j) {
+    const int p = (S.rr + j) % P;
+    const int st = S.st[p];
+    if (st != ST_RUN && st != ST_FINAL) continue;
+    const int K = S.K[p];
+    if (nc + K > CW || ni + 1 > IMAX) {
+      if (first_skip < 0) first_skip = p;
+      continue;
+    }
+    S.pitem[p] = static_cast<short>(ni);
+    S.ikind[ni] = static_cast<unsigned char>(st == ST_RUN ? IK_RUN : IK_FINAL);
+    S.iprob[ni] = static_cast<unsigned char>(p);
+    S.ioff[ni] = static_cast<short>(nc);
+    S.incol[ni] = static_cast<short>(K);
+    S.itr[ni] = 0;
+    for (int c = 0; c < K; ++c) {
+      S.sitem[nc + c] = static_cast<short>(ni);
+      S.scl[nc + c] = static_cast<short>(st == ST_RUN ? c : -1);
+      S.srow[nc + c] = -(S.cenoff[p] + c) - 1;
+    }
+    ++ni;
+    nc += K;
+    last = p;
+    nlloyd += static_cast<unsigned long long>(K) * a.m;
+    if (st == ST_RUN) nm += a.m;
+  }
+  S.rr = (first_skip >= 0) ? first_skip : (last >= 0 ? (last + 1) % P : S.rr);
+  S.nitems = ni;
+  S.ncols = nc;
+  S.n_seed += nseed;
+  S.n_lloyd += nlloyd;
+  S.n_mrows += nm;
+  if (ni > 0) {
+    S.n_sweeps += 1;
+    S.n_ctiles += static_cast<unsigned long long>((nc + 31) / 32) * a.T;
+  }
+}
+
 template <int DP>
 __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
   using LY = Lay<DP>;
   __shared__ __attribute__((aligned(16))) char smem[LY::TOTAL];
-  float* Xr = reinterpret_cast<float*>(smem);                 // 3-slot tile ring
-  float* Ds = reinterpret_cast<float*>(smem + LY::OFF_D);     // distance tile
-  float* Co = reinterpret_cast<float*>(smem + LY::OFF_CO);    // old centres (sweep end)
-  float* Sm = reinterpret_cast<float*>(smem);                 // sums / new centres (aliases ring)
+  char* ring = smem;
+  float* Dt = reinterpret_cast<float*>(smem + LY::OFF_D);   // [2][RT][DSD]
+  float* Sm = reinterpret_cast<float*>(smem);               // [CW][DP] sums (aliases ring + D)
   uint8_t* Ls = reinterpret_cast<uint8_t*>(smem + LY::OFF_LS);
+  float* XN = reinterpret_cast<float*>(smem + LY::OFF_XN);
   State& S = *reinterpret_cast<State*>(smem + LY::OFF_ST);
 
   const int tid = threadIdx.x, lane = tid & 63;
-  // wave index made provably uniform, so the role branches below are scalar branches
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool mrole = wave < 4;      // MFMA waves 0-3, VALU waves 4-7 (one of each per SIMD)
-  const int ct = wave;              // MFMA role: centroid column tile
-  const int vt = tid - NVT;         // VALU role: 0..255
-  const int g = blockIdx.x / a.nh;  // heavy groups (planned first) dispatch first
-  const int hb = blockIdx.x - g * a.nh;
-  const int h = a.h_begin + hb;
-  const int m = a.m;
-  const int T = (m + RT - 1) / RT;
-  const int32_t* idx = a.idx + static_cast<size_t>(h) * m;
-  const int32_t* gd = a.groups + g * GS;
+  const int m = a.m, T = a.T;
   uint8_t* wsb = a.ws + static_cast<size_t>(blockIdx.x) * a.ws_per_wg;
-  uint8_t* glab = wsb;                                           // [Pws][m]
-  float* dbuf = reinterpret_cast<float*>(wsb + a.off_dbuf);      // [Pws][Tws+1][m]
-  int32_t* cpos = reinterpret_cast<int32_t*>(wsb + a.off_cpos);  // [Pws][Kws]
+  uint8_t* glab = wsb;                                                  // [Pws][m]
+  float* cen = reinterpret_cast<float*>(wsb + a.off_cen);               // [Cws][DP]
+  float* cenn = reinterpret_cast<float*>(wsb + a.off_cenn);             // [Cws]
+  int32_t* cpos = reinterpret_cast<int32_t*>(wsb + a.off_cpos);         // [Pws][Kws]
+  float* dbuf = reinterpret_cast<float*>(wsb + a.off_dbuf);             // [seedmax][Tws+1][m]
+  double* tsum = reinterpret_cast<double*>(wsb + a.off_tsum);           // [seedmax][Tws][T]
+  float* rdist = reinterpret_cast<float*>(wsb + a.off_rdist);           // [m]
   const int T1 = a.Tws + 1;
-
-  // ---- problem table --------------------------------------------------------
-  if (tid == 0) {
-    const int P = gd[0];
-    S.P = P;
-    int kg = 0;
-    for (int p = 0; p < P; ++p) {
-      S.K[p] = gd[1 + 4 * p];
-      S.kidx[p] = gd[2 + 4 * p];
-      S.init[p] = gd[3 + 4 * p];
-      S.ntr[p] = gd[4 + 4 * p];
-      S.cs[p] = a.Tws;
-      kg = max(kg, S.K[p]);
-    }
-    S.Kg = kg;
-    S.n_lloyd = S.n_seed = S.n_mrows = S.n_reloc = 0;
-  }
-  __syncthreads();
-  const int P = S.P;
-
-  // ---- tol = tol_rel * mean(var(X_sub, axis=0)) (sklearn _tolerance, :270-278) --
-  {
-    double* red = reinterpret_cast<double*>(Xr);  // [NT/DP][DP]
-    double* mean = reinterpret_cast<double*>(Xr) + NT;
-    constexpr int NPH = NT / DP;
-    const int d = tid % DP, ph = tid / DP;
-    double s = 0.0;
-    for (int r = ph; r < m; r += NPH) s += static_cast<double>(a.X[static_cast<size_t>(idx[r]) * a.ldx + d]);
-    red[ph * DP + d] = s;
-    __syncthreads();
-    if (tid < DP) {
-      double t = 0.0;
-      for (int k = 0; k < NPH; ++k) t += red[k * DP + tid];
-      mean[tid] = t / m;
-    }
-    __syncthreads();
-    const double mu = mean[d];
-    double q = 0.0;
-    for (int r = ph; r < m; r += NPH) {
-      const double v = static_cast<double>(a.X[static_cast<size_t>(idx[r]) * a.ldx + d]) - mu;
-      q += v * v;
-    }
-    __syncthreads();
-    red[ph * DP + d] = q;
-    __syncthreads();
-    if (tid == 0) {
-      double tot = 0.0;
-      for (int dd = 0; dd < a.dreal; ++dd) {
-        double t = 0.0;
-        for (int k = 0; k < NPH; ++k) t += red[k * DP + dd];
-        tot += t / m;
-      }
-      S.tol = static_cast<float>(static_cast<float>(tot / a.dreal) * a.tol_rel);
-    }
-    __syncthreads();
-  }
-
-  // ---- k-means++ seeding (all problems of the group in lockstep over centres c) ----
-  for (int c = 0; c < S.Kg; ++c) {
-    if (c > 0) {
-      // candidates: searchsorted(cumsum_f64(closest), u * pot) per problem, one wave each
-      for (int p = wave; p < P; p += NW) {
-        if (S.K[p] <= c) continue;
-        const int ntr = S.ntr[p];
-        const double* u = a.kpp_u +
-                          (static_cast<size_t>(S.kidx[p]) * a.n_init + S.init[p]) * a.kpp_stride +
-                          1 + static_cast<size_t>(c - 1) * ntr;
-        const double pot = static_cast<double>(S.pot32[p]);
-        double rv[TMAX];
-        unsigned cntv[TMAX];
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-          rv[t] = (t < ntr) ? u[t] * pot : 0.0;
-          cntv[t] = 0;
-        }
-        const float* cl = dbuf + (static_cast<size_t>(p) * T1 + S.cs[p]) * m;
-        double run = 0.0;
-        for (int r0 = 0; r0 < m; r0 += 64) {
-          const int r = r0 + lane;
-          const bool ok = r < m;
-          double v = ok ? static_cast<double>(cl[r]) : 0.0;
-#pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const double y = __shfl_up(v, o);
-            if (lane >= o) v += y;
-          }
-          const double cum = run + v;
-#pragma unroll
-          for (int t = 0; t < TMAX; ++t)
-            if (t < ntr) cntv[t] += static_cast<unsigned>(__popcll(__ballot(ok && cum < rv[t])));
-          run = __shfl(cum, 63);
-        }
-        if (lane == 0)
-#pragma unroll
-          for (int t = 0; t < TMAX; ++t)
-            if (t < ntr) S.cand[p][t] = min(static_cast<int>(cntv[t]), m - 1);
-      }
-    } else if (tid < P) {
-      S.cand[tid][0] = a.kpp_pos[S.kidx[tid] * a.n_init + S.init[tid]];
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int j = 0;
-      for (int p = 0; p < P; ++p) {
-        if (S.K[p] <= c) continue;
-        const int nt = (c == 0) ? 1 : S.ntr[p];
-        S.colbase[p] = j;
-        for (int t = 0; t < nt; ++t) {
-          S.colprob[j] = static_cast<short>(p);
-          S.coltr[j] = static_cast<short>(t);
-          S.colrow[j] = idx[S.cand[p][t]];
-          ++j;
-        }
-      }
-      S.ncols = j;
-      S.colmask = (1u << ((j + 31) / 32)) - 1u;
-      S.n_seed += static_cast<unsigned long long>(j) * m;
-    }
-    __syncthreads();
-    const int ncols = S.ncols;
-    // Role-split pipeline (same barrier count on both sides): the MFMA waves keep the
-    // candidate fragments live, the VALU waves keep the potential partial live.
-    if (mrole) {
-      float4 cf[DP / 8];
-      const bool active = (S.colmask >> ct) & 1;
-      const int col = ct * 32 + (lane & 31);
-      const bool ok = col < ncols;
-      frag_load<DP>(cf, a.X + static_cast<size_t>(ok ? S.colrow[col] : 0) * a.ldx, ok, lane);
-      __syncthreads();
-      for (int t = 0; t <= T; ++t) {
-        v16f acc = {};
-        if (active && t < T) mfma_dims<DP, 0, DP / 16>(cf, Xr + (t % 3) * LY::XBUF, acc, lane);
-        __syncthreads();
-        if (active && t < T) {
-          mfma_dims<DP, DP / 16, DP / 8>(cf, Xr + (t % 3) * LY::XBUF, acc, lane);
-          store_dist(acc, S, Ds, ct, lane);
-        }
-        __syncthreads();
-      }
-    } else {
-      if (vt < CMAX) S.cnorm[vt] = (vt < ncols) ? a.xnorm[S.colrow[vt]] : 0.f;
-      {
-        TileRegs<DP> R;
-        tile_issue<DP>(a, idx, 0, vt, R);
-        tile_commit<DP>(Xr, S.xn[0], vt, R);
-      }
-      __syncthreads();
-      // candidate potentials: thread = (column j, half tile of 16 rows)
-      const int j = vt & (CMAX - 1), rh = vt >> 7;
-      const bool jok = j < ncols;
-      int p = 0, cs = 0, slot = 0;
-      if (jok) {
-        p = S.colprob[j];
-        cs = S.cs[p];
-        const int tr = S.coltr[j];
-        slot = (tr < cs) ? tr : tr + 1;
-      }
-      const float* closest = dbuf + (static_cast<size_t>(p) * T1 + cs) * m;
-      float* dout = dbuf + (static_cast<size_t>(p) * T1 + slot) * m;
-      double pacc = 0.0;
-      for (int t = 0; t <= T; ++t) {
-        int vtl = vt;
-        asm volatile("" : "+v"(vtl));
-        TileRegs<DP> R;
-        if (t + 1 < T) tile_issue<DP>(a, idx, (t + 1) * RT, vtl, R);
-        if (t >= 1 && jok) {
-          const float* xnr = S.xn[(t - 1) % 3];
-          const int rb = (t - 1) * RT + rh * 16;
-          float cl[16];  // branch-free: clamped rows, value unused when c == 0 or past m
-#pragma unroll
-          for (int q = 0; q < 16; ++q) cl[q] = closest[min(rb + q, m - 1)];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int rr = rh * 16 + q;
-            if (rb + q < m) {
-              const float dist = fmaxf(xnr[rr] + Ds[rr * DSD + j], 0.f);
-              const float dmin = (c == 0) ? dist : fminf(cl[q], dist);
-              dout[rb + q] = dmin;
-              pacc += static_cast<double>(dmin);
-            }
-          }
-        }
-        if (t + 1 < T) tile_commit<DP>(Xr + ((t + 1) % 3) * LY::XBUF, S.xn[(t + 1) % 3], vtl, R);
-        __syncthreads();
-        __syncthreads();
-      }
-      if (jok) (rh ? S.potc2 : S.potc)[j] = pacc;
-    }
-    __syncthreads();
-    if (tid < ncols) S.potc[tid] += S.potc2[tid];
-    __syncthreads();
-    if (tid < P && S.K[tid] > c) {
-      const int p = tid, j0 = S.colbase[p];
-      const int nt = (c == 0) ? 1 : S.ntr[p];
-      int best = 0;
-      float bv = static_cast<float>(S.potc[j0]);
-      for (int t = 1; t < nt; ++t) {
-        const float v = static_cast<float>(S.potc[j0 + t]);
-        if (v < bv) {
-          bv = v;
-          best = t;
-        }
-      }
-      S.pot32[p] = bv;
-      S.cs[p] = (best < S.cs[p]) ? best : best + 1;
-      cpos[p * a.Kws + c] = S.cand[p][best];
-    }
-    __syncthreads();
-  }
-
-  // ---- Lloyd ------------------------------------------------------------------
-  if (tid == 0) {
-    int o = 0;
-    for (int p = 0; p < P; ++p) {
-      S.off[p] = o;
-      for (int c = 0; c < S.K[p]; ++c) {
-        S.colprob[o + c] = static_cast<short>(p);
-        S.colrow[o + c] = idx[cpos[p * a.Kws + c]];
-      }
-      o += S.K[p];
-      S.st[p] = ST_RUN;
-      S.iter[p] = 0;
-    }
-    S.ncols = o;
-  }
-  for (size_t e = tid; e < static_cast<size_t>(P) * m; e += NT) glab[e] = 0xFF;
-  __syncthreads();
-  const int ncols = S.ncols;
-  // initial centres (the seeded rows) -> Sm, their norms
-  for (int e = tid; e < CMAX * (DP / 4); e += NT) {
-    const int col = e / (DP / 4), c4 = e - col * (DP / 4);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (col < ncols) v = *reinterpret_cast<const float4*>(a.X + static_cast<size_t>(S.colrow[col]) * a.ldx + 4 * c4);
-    *reinterpret_cast<float4*>(Sm + col * DP + 4 * c4) = v;
-  }
-  if (tid < CMAX) S.cnorm[tid] = (tid < ncols) ? row_sq(a.X + static_cast<size_t>(S.colrow[tid]) * a.ldx, a.dreal) : 0.f;
-  if (tid < PMAX) S.changed[tid] = 0;
-  __syncthreads();
+  if (tid == 0) S.n_lloyd = S.n_seed = S.n_mrows = S.n_reloc = S.n_sweeps = S.n_ctiles = 0;
 
   for (;;) {
+    __syncthreads();
+    if (tid == 0) S.unit = static_cast<int>(atomicAdd(a.counter, 1u));
+    __syncthreads();
+    const int unit = S.unit;
+    if (unit >= a.nh * a.nU) break;
+    const int hb = unit / a.nU, g = unit - hb * a.nU;
+    const int h = a.h_begin + hb;
+    const int32_t* idx = a.idx + static_cast<size_t>(h) * m;
+    const int32_t* gd = a.units + g * US;
+
+    // ---- problem table --------------------------------------------------------
     if (tid == 0) {
-      unsigned msk = 0;
-      int any = 0;
-      unsigned long long work = 0, mrows = 0;
+      const int P = gd[0];
+      S.P = P;
+      int o = 0;
       for (int p = 0; p < P; ++p) {
-        const int st = S.st[p];
-        if (st == ST_RUN || st == ST_FINAL) {
-          any = 1;
-          for (int q = S.off[p] / 32; q <= (S.off[p] + S.K[p] - 1) / 32; ++q) msk |= 1u << q;
-          work += static_cast<unsigned long long>(S.K[p]) * m;
-          if (st == ST_RUN) mrows += m;
-        }
+        S.K[p] = static_cast<unsigned char>(gd[1 + 4 * p]);
+        S.kidx[p] = static_cast<unsigned char>(gd[2 + 4 * p]);
+        S.init[p] = static_cast<unsigned char>(gd[3 + 4 * p]);
+        S.ntr[p] = static_cast<unsigned char>(gd[4 + 4 * p]);
+        S.st[p] = ST_WAIT;
+        S.iter[p] = 0;
+        S.cenoff[p] = static_cast<short>(o);
+        o += S.K[p];
       }
-      S.colmask = static_cast<int>(msk);
-      S.any = any;
-      S.n_lloyd += work;
-      S.n_mrows += mrows;
+      S.rr = 0;
+      S.seedfree = (a.seedmax >= 32) ? 0xFFFFFFFFu : ((1u << a.seedmax) - 1u);
     }
     __syncthreads();
-    if (!S.any) break;
+    const int P = S.P;
+    for (size_t e = tid; e < static_cast<size_t>(P) * m; e += NT) glab[e] = 0xFF;
 
-    // Role-split sweep: both sides execute 2 + 2*(T+1) barriers.
-    if (mrole) {
-      float4 cf[DP / 8];  // register-resident centres of column tile ct
-      const bool active = (S.colmask >> ct) & 1;
-      const int col = ct * 32 + (lane & 31);
-      frag_load<DP>(cf, Sm + col * DP, true, lane);
-      __syncthreads();  // B0: fragments read, Sm may be cleared
-      __syncthreads();  // B1: tile 0 in the ring
-#ifdef CC_KM_STAMPS
-      unsigned long long st_acc[4] = {0, 0, 0, 0};
-#endif
-      for (int t = 0; t <= T; ++t) {
-        KM_STAMP(s0);
-        v16f acc = {};
-        if (active && t < T) mfma_dims<DP, 0, DP / 16>(cf, Xr + (t % 3) * LY::XBUF, acc, lane);
-        KM_STAMP(s1);
-        __syncthreads();
-        KM_STAMP(s2);
-        if (active && t < T) {
-          mfma_dims<DP, DP / 16, DP / 8>(cf, Xr + (t % 3) * LY::XBUF, acc, lane);
-          store_dist(acc, S, Ds, ct, lane);
-        }
-        KM_STAMP(s3);
-        __syncthreads();
-        KM_STAMP(s4);
-        KM_ACC(0, s0, s1);
-        KM_ACC(1, s1, s2);
-        KM_ACC(2, s2, s3);
-        KM_ACC(3, s3, s4);
+    // ---- tol = tol_rel * mean(var(X_sub, axis=0)) (sklearn _tolerance, :270-278) --
+    {
+      double* red = reinterpret_cast<double*>(ring);  // [NT/DP][DP]
+      double* mean = reinterpret_cast<double*>(ring) + NT;
+      constexpr int NPH = NT / DP;
+      const int d = tid % DP, ph = tid / DP;
+      double s = 0.0;
+      for (int r = ph; r < m; r += NPH) s += static_cast<double>(a.X[static_cast<size_t>(idx[r]) * DP + d]);
+      red[ph * DP + d] = s;
+      __syncthreads();
+      if (tid < DP) {
+        double t = 0.0;
+        for (int k = 0; k < NPH; ++k) t += red[k * DP + tid];
+        mean[tid] = t / m;
       }
-#ifdef CC_KM_STAMPS
-      if (blockIdx.x == 0 && lane == 0 && a.stats)
-        for (int k = 0; k < 4; ++k) atomicAdd(&a.stats[4 + 4 * wave + k], st_acc[k]);
-#endif
-      // old centres -> Co
-      float* co = Co + col * DP + 4 * (lane >> 5);
+      __syncthreads();
+      const double mu = mean[d];
+      double q = 0.0;
+      for (int r = ph; r < m; r += NPH) {
+        const double v = static_cast<double>(a.X[static_cast<size_t>(idx[r]) * DP + d]) - mu;
+        q += v * v;
+      }
+      __syncthreads();
+      red[ph * DP + d] = q;
+      __syncthreads();
+      if (tid == 0) {
+        double tot = 0.0;
+        for (int dd = 0; dd < a.dreal; ++dd) {
+          double t = 0.0;
+          for (int k = 0; k < NPH; ++k) t += red[k * DP + dd];
+          tot += t / m;
+        }
+        S.tol = static_cast<float>(static_cast<float>(tot / a.dreal) * a.tol_rel);
+      }
+      __syncthreads();
+    }
+
+    // ---- sweeps -----------------------------------------------------------------
+    for (;;) {
+      if (tid == 0) schedule(a, S, idx);
+      __syncthreads();
+      const int nitems = S.nitems, ncols = S.ncols;
+      if (nitems == 0) break;
+
+      // slot norms: centres from the last write-back, candidates from xnorm
+      if (tid < ncols) {
+        const int sr = S.srow[tid];
+        S.cnorm[tid] = (sr >= 0) ? a.xnorm[sr] : cenn[-sr - 1];
+      }
+      // Every wave owns the slot tile ct = wave (32 slots): its centres as register-resident
+      // f16 A fragments (distances) and its M-step sums as MFMA accumulators.
+      const int ct = wave;
+      const int hh = lane >> 5, lr = lane & 31;
+      const int sl = 32 * ct + lr;
+      EState es;
+      es.chmask = 0;
 #pragma unroll
-      for (int s = 0; s < DP / 8; ++s) *reinterpret_cast<float4*>(co + 8 * s) = cf[s];
-    } else {
-      __syncthreads();  // B0
+      for (int i = 0; i < NS; ++i) es.iacc[i] = 0.0;
+      h8 ah[DP / 16], al[DP / 16];
+      const bool tact = 32 * ct < ncols;  // wave-uniform
+      {
+        int sr = 0;
+        if (sl < ncols) sr = S.srow[sl];
+        const float* src = (sr >= 0) ? a.X + static_cast<size_t>(sr) * DP : cen + static_cast<size_t>(-sr - 1) * DP;
+        afrag_load<DP>(ah, al, src, sl < ncols, hh, a.scale);
+      }
+      v16f sacc[DP / 32];
+#pragma unroll
+      for (int dt = 0; dt < DP / 32; ++dt) sacc[dt] = v16f{};
+      unsigned mcnt = 0;
+      int mycl = -1, myit = 0;
+      if (sl < ncols) {
+        myit = S.sitem[sl];
+        mycl = S.scl[sl];
+      }
+      const bool mact = __ballot(mycl >= 0) != 0ull;  // wave-uniform: any running centre
       {
         TileRegs<DP> R;
-        tile_issue<DP>(a, idx, 0, vt, R);
-        tile_commit<DP>(Xr, S.xn[0], vt, R);
+        tile_issue<DP>(a, idx, 0, tid, R);
+        tile_commit<DP>(ring, XN, tid, R);
       }
-      __syncthreads();  // B1
-      constexpr int NS = PMAX / NW;  // E-step slots per thread: problems ps + 8i
-      double iacc[NS];
-      unsigned chmask = 0;  // bit i: a label of problem ps + 8i changed in this sweep
-      const int row0 = vt & 31, ps = vt >> 5;
-      int sK[NS], soff[NS], sst[NS];
-#pragma unroll
-      for (int i = 0; i < NS; ++i) {
-        iacc[i] = 0.0;
-        const int p = ps + NW * i;
-        sst[i] = (p < P) ? S.st[p] : ST_IDLE;
-        sK[i] = (p < P) ? S.K[p] : 0;
-        soff[i] = (p < P) ? S.off[p] : 0;
-      }
-      // M-step role: this wave owns centroid column tile mct, all dims (NDT tiles), counts
-      constexpr int NDT = DP / 32;
-      const int mct = wave - 4;
-      const int mcol = mct * 32 + (lane & 31);
-      int mcl = -1, mpc = 0;
-      if (mcol < ncols) {
-        mpc = S.colprob[mcol];
-        if (S.st[mpc] == ST_RUN) mcl = mcol - S.off[mpc];
-      }
-      const bool mact = __ballot(mcl >= 0) != 0ull;  // wave-uniform: any running column
-      v16f sacc[NDT], cacc = {};
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) sacc[dt] = v16f{};
-      const u32x4 ones = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
-#ifdef CC_KM_STAMPS
-      unsigned long long st_acc[4] = {0, 0, 0, 0};
-#endif
-      for (int t = 0; t <= T; ++t) {
-        KM_STAMP(s0);
-        // Opaque copies: keep the compiler from hoisting (and spilling) every per-slot and
-        // per-element address out of the tile loop; they are cheap to recompute.
-        int row = row0, vtl = vt;
-        asm volatile("" : "+v"(row), "+v"(vtl));
-        // phase 1: gather tile t+1 | E-step of tile t-1
+      __syncthreads();
+      for (int t = 0; t <= T + 1; ++t) {
+        int tidl = tid;
+        asm volatile("" : "+v"(tidl));
         TileRegs<DP> R;
-        if (t + 1 < T) tile_issue<DP>(a, idx, (t + 1) * RT, vtl, R);
-        if (t >= 1) {
-          const int r = (t - 1) * RT + row;
-          const bool ok = r < m;
-          const float xnr = S.xn[(t - 1) % 3][row];
-          uint8_t old[NS];
+        if (t + 1 < T) tile_issue<DP>(a, idx, (t + 1) * RT, tidl, R);
+        unsigned pre[NS];
+        estep_prefetch(a, S, t, T, nitems, tidl, glab, dbuf, T1, pre);
+        // distances of tile t (MFMA) -> D[t & 1]
+        if (tact && t < T) {
+          const char* xs = ring + (t % NRING) * LY::SLOT;
+          v16f acc = {};
 #pragma unroll
-          for (int i = 0; i < NS; ++i)
-            old[i] = (ok && sst[i] == ST_RUN) ? glab[static_cast<size_t>(ps + NW * i) * m + r] : 0;
+          for (int s = 0; s < DP / 16; ++s) {
+            const int off = xoff<DP>(lr, 2 * s + hh);
+            const h8 bh = *reinterpret_cast<const h8*>(xs + off);
+            const h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
+            acc = mfma16(ah[s], bl, acc);
+            acc = mfma16(al[s], bh, acc);
+            acc = mfma16(ah[s], bh, acc);
+            if (s & 1) __builtin_amdgcn_sched_barrier(0);  // bound the B operands in flight
+          }
+          float* drow = Dt + (t & 1) * (RT * DSD) + lr * DSD + 32 * ct + 4 * hh;
+          const float* cn = S.cnorm + 32 * ct + 4 * hh;
 #pragma unroll
-          for (int i = 0; i < NS; ++i) {
-            if (sst[i] != ST_RUN && sst[i] != ST_FINAL) continue;
-            const int p = ps + NW * i;
-            const float* drow = Ds + row * DSD + soff[i];
-            const int K = sK[i];
-            float best = drow[0];
-            int lab = 0;
-            for (int c0 = 1; c0 < K; c0 += 8) {  // 8 loads in flight, then strict-< scan
-              float v[8];
-#pragma unroll
-              for (int j = 0; j < 8; ++j) v[j] = drow[min(c0 + j, K - 1)];
-#pragma unroll
-              for (int j = 0; j < 8; ++j)
-                if (c0 + j < K && v[j] < best) {
-                  best = v[j];
-                  lab = c0 + j;
-                }
-            }
-            if (ok) {
-              if (sst[i] == ST_RUN && old[i] != static_cast<uint8_t>(lab)) chmask |= 1u << i;
-              glab[static_cast<size_t>(p) * m + r] = static_cast<uint8_t>(lab);
-              iacc[i] += static_cast<double>(xnr) + static_cast<double>(best);
-            }
-            Ls[p * RT + row] = ok ? static_cast<uint8_t>(lab) : 0xFF;
+          for (int v = 0; v < 16; ++v) {
+            const int i = (v & 3) + 8 * (v >> 2);
+            drow[i] = cn[i] - a.dscale * acc[v];
           }
         }
-        if (t + 1 < T) tile_commit<DP>(Xr + ((t + 1) % 3) * LY::XBUF, S.xn[(t + 1) % 3], vtl, R);
-        KM_STAMP(s1);
-        __syncthreads();
-        KM_STAMP(s2);
-        // phase 2: M-step of tile t-1 on bf16 MFMA (one-hot A, bf16x3 rows B, ones for counts)
-        if (t >= 1 && mact) {
-          const float* Xb = Xr + ((t - 1) % 3) * LY::XBUF + (lane & 31);
-          const int g8 = 8 * (lane >> 5);
-          constexpr int NQ = (RT / 16) * NDT;  // (k-step, dim tile) pairs
-          float xc[8], xn8[8];
+        estep<DP>(a, S, t, T, nitems, tidl, Dt, Ls, XN, glab, dbuf, tsum, T1, pre, es);
+        // M-step of tile t-2 (one-hot x X on f16 MFMA; counts by popcount)
+        if (mact && t >= 2) {
+          const int tm = t - 2;
+          const char* xs = ring + (tm % NRING) * LY::SLOT;
+          const uint8_t* lsb = Ls + (tm & 1) * (IMAX * RT) + myit * RT;
+          int lanel = lane;
+          asm volatile("" : "+v"(lanel));
+          const int G = lanel >> 4, q = (lanel >> 2) & 3, pp = lanel & 3;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) xc[j] = Xb[(g8 + j) * LY::XS];
-          u32x4 afr;
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const unsigned long long lab8 = *reinterpret_cast<const unsigned long long*>(lsb + 16 * s2 + 8 * hh);
+            u32x4 ohu;
+            unsigned nb = 0;
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) {
-            const int ks = q / NDT, dt = q - (q / NDT) * NDT;
-            if (q + 1 < NQ) {  // prefetch the next (k-step, dim tile) rows
-              const int ks1 = (q + 1) / NDT, dt1 = (q + 1) - ((q + 1) / NDT) * NDT;
-#pragma unroll
-              for (int j = 0; j < 8; ++j) xn8[j] = Xb[(16 * ks1 + g8 + j) * LY::XS + dt1 * 32];
+            for (int j = 0; j < 4; ++j) {
+              const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
+              const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
+              ohu[j] = ((b0 == mycl) ? 0x3C00u : 0u) | ((b1 == mycl) ? 0x3C000000u : 0u);
+              nb += (b0 == mycl) + (b1 == mycl);
             }
-            if (dt == 0) {  // one-hot of this lane's column over its 8 rows of k-step ks
-              const unsigned long long lab8 =
-                  *reinterpret_cast<const unsigned long long*>(Ls + mpc * RT + 16 * ks + g8);
+            mcnt += nb;
+            const h8 oh = __builtin_bit_cast(h8, ohu);
+            const int row0 = 16 * s2 + 8 * (G >> 1) + q;
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
-                const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
-                afr[j] = ((b0 == mcl) ? 0x3F80u : 0u) | ((b1 == mcl) ? 0x3F800000u : 0u);
-              }
-              cacc = mfma_bf16(afr, ones, cacc);
+            for (int dt = 0; dt < DP / 32; ++dt) {
+              const int chn = 4 * dt + 2 * (G & 1) + (pp >> 1);
+              const int a0 = xoff<DP>(row0, chn) + 8 * (pp & 1);
+              const int a1 = xoff<DP>(row0 + 4, chn) + 8 * (pp & 1);
+              const s4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a0));
+              const s4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a1));
+              const s4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a0));
+              const s4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a1));
+              const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
+              const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7));
+              sacc[dt] = mfma16(oh, bl, sacc[dt]);
+              sacc[dt] = mfma16(oh, bh, sacc[dt]);
+              __builtin_amdgcn_sched_barrier(0);
             }
-            u32x4 f0, f1, f2;
-            split3(xc, f0, f1, f2);
-            sacc[dt] = mfma_bf16(afr, f0, sacc[dt]);
-            sacc[dt] = mfma_bf16(afr, f1, sacc[dt]);
-            sacc[dt] = mfma_bf16(afr, f2, sacc[dt]);
-            __builtin_amdgcn_sched_barrier(0);  // bound the live split fragments
-#pragma unroll
-            for (int j = 0; j < 8; ++j) xc[j] = xn8[j];
           }
         }
-        KM_STAMP(s3);
-        __syncthreads();
-        KM_STAMP(s4);
-        KM_ACC(0, s0, s1);
-        KM_ACC(1, s1, s2);
-        KM_ACC(2, s2, s3);
-        KM_ACC(3, s3, s4);
-      }
-#ifdef CC_KM_STAMPS
-      if (blockIdx.x == 0 && (vt & 63) == 0 && a.stats)
-        for (int k = 0; k < 4; ++k) atomicAdd(&a.stats[4 + 4 * wave + k], st_acc[k]);
-#endif
-#pragma unroll
-      for (int i = 0; i < PMAX / NW; ++i) {
-        const int p = ps + NW * i;
-        if (p < P) {
-          const double v = half_sum(iacc[i]);
-          if (row0 == 0) S.sweep_inert[p] = v;
-          if ((chmask >> i) & 1u) S.changed[p] = 1;
-        }
-      }
-      // sums -> Sm (aliases the ring: every ring reader passed the last barrier) ; counts
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int c = mct * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-          Sm[c * DP + dt * 32 + (lane & 31)] = sacc[dt][v];
-        }
-      if ((lane & 31) == 0)
-#pragma unroll
-        for (int v = 0; v < 16; ++v)
-          S.cnt[mct * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5)] = static_cast<unsigned>(cacc[v]);
-    }
-    if (tid == 0) {
-      int f = 0;
-      for (int p = 0; p < P; ++p) {
-        S.nempty[p] = 0;
-        if (S.st[p] != ST_RUN) continue;
-        for (int c = 0; c < S.K[p]; ++c) S.nempty[p] += (S.cnt[S.off[p] + c] == 0);
-        f |= (S.nempty[p] > 0);
-      }
-      S.flag = f;
-    }
-    __syncthreads();
-    if (S.flag) {
-      for (int p = 0; p < P; ++p) {
-        if (S.nempty[p] == 0) continue;
-        relocate<DP>(a, idx, p, Co, Sm, S, glab, dbuf + static_cast<size_t>(p) * T1 * m, tid);
+        if (t + 1 < T) tile_commit<DP>(ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * RT, tidl, R);
         __syncthreads();
       }
-    }
-    // first argmax of counts per problem (for clusters still empty: _average_centers)
-    if (tid < P && S.st[tid] == ST_RUN) {
-      const int off = S.off[tid];
-      int am = 0;
-      for (int c = 1; c < S.K[tid]; ++c)
-        if (S.cnt[off + c] > S.cnt[off + am]) am = c;
-      S.amax[tid] = am;
-    }
-    __syncthreads();
-    // _average_centers (_k_means_common.pyx:215-237) runs j in order: an empty cluster
-    // j copies centre argmax(weight), which is still a raw sum when j < argmax.
-    for (int e = tid; e < ncols * DP; e += NT) {
-      const int col = e / DP, d = e - col * DP;
-      const int p = S.colprob[col];
-      if (S.st[p] != ST_RUN || S.cnt[col] != 0 || col - S.off[p] > S.amax[p]) continue;
-      Sm[col * DP + d] = Sm[(S.off[p] + S.amax[p]) * DP + d];
-    }
-    __syncthreads();
-    for (int e = tid; e < ncols * DP; e += NT) {
-      const int col = e / DP;
-      const int p = S.colprob[col];
-      if (S.st[p] != ST_RUN) continue;
-      const unsigned cn = S.cnt[col];
-      if (cn > 0) {
-        const float alpha = static_cast<float>(1.0 / static_cast<double>(static_cast<float>(cn)));
-        Sm[e] *= alpha;
+      estep_finish(S, nitems, tid, es);
+      // sums -> Sm (aliases the ring and D: every reader passed the last barrier); counts
+      if (mact) {
+#pragma unroll
+        for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const int s2 = 32 * ct + (v & 3) + 8 * (v >> 2) + 4 * hh;
+            Sm[s2 * DP + 32 * dt + lr] = sacc[dt][v] * a.inv_scale;
+          }
+        const unsigned tot = mcnt + __shfl_xor(mcnt, 32);
+        if (hh == 0) S.cnt[sl] = tot;
       }
-    }
-    __syncthreads();
-    for (int e = tid; e < ncols * DP; e += NT) {
-      const int col = e / DP, d = e - col * DP;
-      const int p = S.colprob[col];
-      if (S.st[p] != ST_RUN || S.cnt[col] != 0 || col - S.off[p] < S.amax[p]) continue;
-      Sm[col * DP + d] = Sm[(S.off[p] + S.amax[p]) * DP + d];
-    }
-    __syncthreads();
-    // centre shifts (sklearn _euclidean_dense_dense, 4-way unrolled f32)
-    if (tid < ncols && S.st[S.colprob[tid]] == ST_RUN) {
-      const float* cn = Sm + tid * DP;
-      const float* co = Co + tid * DP;
-      float res = 0.f;
-      const int n4 = a.dreal / 4, rem = a.dreal % 4;
-      for (int i = 0; i < n4; ++i) {
-        const float d0 = cn[4 * i] - co[4 * i], d1 = cn[4 * i + 1] - co[4 * i + 1];
-        const float d2 = cn[4 * i + 2] - co[4 * i + 2], d3 = cn[4 * i + 3] - co[4 * i + 3];
-        res += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
-      }
-      for (int i = 0; i < rem; ++i) {
-        const float dd = cn[4 * n4 + i] - co[4 * n4 + i];
-        res += dd * dd;
-      }
-      const float sh = sqrtf(res);
-      S.shift[tid] = sh * sh;
-    }
-    __syncthreads();
-    // convergence decisions (_kmeans_single_lloyd :697-736)
-    if (tid < P) {
-      const int p = tid;
-      const int st = S.st[p];
-      if (st == ST_RUN) {
-        S.iter[p] += 1;
-        if (!S.changed[p]) {
-          S.st[p] = ST_DONE;  // strict convergence: final labels and centres are this sweep's
-          S.inert[p] = static_cast<float>(S.sweep_inert[p]);
-        } else {
-          const float tot = np_pairwise_sum(S.shift + S.off[p], S.K[p]);
-          S.st[p] = (tot <= S.tol || S.iter[p] >= a.max_iter) ? ST_FINAL : ST_RUN;
-        }
-      } else if (st == ST_FINAL) {
-        S.st[p] = ST_DONE;
-        S.inert[p] = static_cast<float>(S.sweep_inert[p]);
-      }
-      S.changed[p] = 0;
-    }
-    __syncthreads();
-    // norms of the centres of problems that sweep again (Sm keeps them for the fragments)
-    if (tid < ncols) {
-      const int st = S.st[S.colprob[tid]];
-      if (st == ST_RUN || st == ST_FINAL) S.cnorm[tid] = row_sq(Sm + tid * DP, a.dreal);
-    }
-    __syncthreads();
-  }
+      __syncthreads();
 
-  // ---- best of n_init per K, output (KMeans.fit :1495-1531) -------------------
-  for (int p0 = 0; p0 < P; p0 += a.n_init) {
-    int best = p0;
-    for (int i = 1; i < a.n_init; ++i) {
-      const int p = p0 + i;
-      if (!(S.inert[p] < S.inert[best])) continue;
-      // _is_same_clustering(labels_p, labels_best): labels_p -> labels_best must be a function
-      if (tid <= KMAX) S.map[tid] = -1;
-      if (tid == 0) S.flag = 0;
+      // ---- seeding decisions (thread per problem) -----------------------------------
+      if (tid < P) {
+        const int p = tid;
+        S.need_sel[p] = 0;
+        S.to_run[p] = 0;
+        if (S.st[p] == ST_SEED && S.pitem[p] >= 0) {
+          const int it0 = S.pitem[p], c = S.c[p];
+          const int nt = (c == 0) ? 1 : S.ntr[p];
+          int best = 0;
+          float bv = static_cast<float>(S.iinert[it0]);
+          for (int t = 1; t < nt; ++t) {
+            const float v = static_cast<float>(S.iinert[it0 + t]);
+            if (v < bv) {
+              bv = v;
+              best = t;
+            }
+          }
+          S.pot32[p] = bv;
+          const int cs = S.cs[p];
+          S.cs[p] = static_cast<unsigned char>((c == 0) ? 0 : ((best < cs) ? best : best + 1));
+          S.sbest[p] = static_cast<unsigned char>(best);
+          cpos[p * a.Kws + c] = (c == 0) ? a.kpp_pos[S.kidx[p] * a.n_init + S.init[p]] : S.cand[p][best];
+          S.c[p] = static_cast<unsigned char>(c + 1);
+          if (c + 1 == S.K[p]) {
+            S.to_run[p] = 1;  // seeding slot released below (single writer)
+          } else {
+            S.need_sel[p] = 1;
+          }
+        }
+      }
       __syncthreads();
-      const uint8_t* l1 = glab + static_cast<size_t>(p) * m;
-      const uint8_t* l2 = glab + static_cast<size_t>(best) * m;
-      for (int r = tid; r < m; r += NT) S.map[l1[r]] = l2[r];
+      if (tid == 0) {
+        for (int p = 0; p < P; ++p)
+          if (S.to_run[p]) {
+            S.seedfree |= 1u << S.sslot[p];
+            S.st[p] = ST_RUN;
+            S.iter[p] = 0;
+          }
+      }
+      // candidate selection: one wave per problem
+      {
+        int j = 0;
+        for (int p = 0; p < P; ++p) {
+          if (!S.need_sel[p]) continue;
+          if ((j++ % NW) != wave) continue;
+          const int ss = S.sslot[p];
+          kpp_select(a, S, p, dbuf + (static_cast<size_t>(ss) * T1 + S.cs[p]) * m,
+                     tsum + (static_cast<size_t>(ss) * a.Tws + S.sbest[p]) * T, lane);
+        }
+      }
+      // initial centres of problems leaving seeding: the chosen rows (exact f32)
+      for (int p = 0; p < P; ++p) {
+        if (!S.to_run[p]) continue;
+        const int K = S.K[p];
+        for (int e = tid; e < K * DP; e += NT) {
+          const int c = e / DP, d = e - c * DP;
+          cen[(S.cenoff[p] + c) * DP + d] = a.X[static_cast<size_t>(idx[cpos[p * a.Kws + c]]) * DP + d];
+        }
+        if (tid < K) cenn[S.cenoff[p] + tid] = row_sq(a.X + static_cast<size_t>(idx[cpos[p * a.Kws + tid]]) * DP, a.dreal);
+      }
+
+      // ---- Lloyd M-step completion (RUN items) ------------------------------------
+      if (tid == 0) {
+        int f = 0;
+        for (int it = 0; it < nitems; ++it) {
+          if (S.ikind[it] != IK_RUN) continue;
+          const int p = S.iprob[it], off = S.ioff[it];
+          int ne = 0;
+          for (int c = 0; c < S.K[p]; ++c) ne += (S.cnt[off + c] == 0);
+          S.nempty[p] = ne;
+          f |= (ne > 0);
+        }
+        S.flag = f;
+      }
       __syncthreads();
-      bool bad = false;
-      for (int r = tid; r < m; r += NT) bad |= (S.map[l1[r]] != l2[r]);
-      if (bad) S.flag = 1;
+      if (S.flag) {
+        for (int it = 0; it < nitems; ++it) {
+          if (S.ikind[it] != IK_RUN) continue;
+          const int p = S.iprob[it];
+          if (S.nempty[p] == 0) continue;
+          relocate<DP>(a, idx, p, S.ioff[it], cen, Sm, S, glab, rdist, tid);
+          __syncthreads();
+        }
+      }
+      // first argmax of counts per problem (for clusters still empty: _average_centers)
+      if (tid < nitems && S.ikind[tid] == IK_RUN) {
+        const int p = S.iprob[tid], off = S.ioff[tid];
+        int am = 0;
+        for (int c = 1; c < S.K[p]; ++c)
+          if (S.cnt[off + c] > S.cnt[off + am]) am = c;
+        S.amax[p] = am;
+      }
       __syncthreads();
-      if (S.flag) best = p;
+      // _average_centers (_k_means_common.pyx:215-237) runs j in order: an empty cluster
+      // j copies centre argmax(weight), which is still a raw sum when j < argmax.
+      for (int e = tid; e < ncols * DP; e += NT) {
+        const int sl = e / DP, d = e - sl * DP;
+        const int it = S.sitem[sl];
+        if (S.ikind[it] != IK_RUN || S.cnt[sl] != 0) continue;
+        const int p = S.iprob[it], off = S.ioff[it];
+        if (sl - off > S.amax[p]) continue;
+        Sm[sl * DP + d] = Sm[(off + S.amax[p]) * DP + d];
+      }
+      __syncthreads();
+      for (int e = tid; e < ncols * DP; e += NT) {
+        const int sl = e / DP;
+        if (S.ikind[S.sitem[sl]] != IK_RUN) continue;
+        const unsigned cn = S.cnt[sl];
+        if (cn > 0) {
+          const float alpha = static_cast<float>(1.0 / static_cast<double>(static_cast<float>(cn)));
+          Sm[e] *= alpha;
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < ncols * DP; e += NT) {
+        const int sl = e / DP, d = e - sl * DP;
+        const int it = S.sitem[sl];
+        if (S.ikind[it] != IK_RUN || S.cnt[sl] != 0) continue;
+        const int p = S.iprob[it], off = S.ioff[it];
+        if (sl - off < S.amax[p]) continue;
+        Sm[sl * DP + d] = Sm[(off + S.amax[p]) * DP + d];
+      }
+      __syncthreads();
+      // centre shifts (sklearn _euclidean_dense_dense, 4-way unrolled f32)
+      if (tid < ncols && S.ikind[S.sitem[tid]] == IK_RUN) {
+        const int sl = tid;
+        const int it = S.sitem[sl];
+        const int p = S.iprob[it];
+        const float* cnw = Sm + sl * DP;
+        const float* co = cen + (S.cenoff[p] + (sl - S.ioff[it])) * DP;
+        float res = 0.f;
+        const int n4 = a.dreal / 4, rem = a.dreal % 4;
+        for (int i = 0; i < n4; ++i) {
+          const float d0 = cnw[4 * i] - co[4 * i], d1 = cnw[4 * i + 1] - co[4 * i + 1];
+          const float d2 = cnw[4 * i + 2] - co[4 * i + 2], d3 = cnw[4 * i + 3] - co[4 * i + 3];
+          res += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+        }
+        for (int i = 0; i < rem; ++i) {
+          const float dd = cnw[4 * n4 + i] - co[4 * n4 + i];
+          res += dd * dd;
+        }
+        const float sh = sqrtf(res);
+        S.shift[sl] = sh * sh;
+      }
+      __syncthreads();
+      // convergence decisions (_kmeans_single_lloyd :697-736)
+      if (tid < nitems && S.ikind[tid] >= IK_RUN) {
+        const int it = tid, p = S.iprob[it];
+        if (S.ikind[it] == IK_RUN) {
+          S.iter[p] += 1;
+          if (!S.ichanged[it]) {
+            S.st[p] = ST_DONE;  // strict convergence: final labels are this sweep's
+            S.inert[p] = static_cast<float>(S.iinert[it]);
+          } else {
+            const float tot = np_pairwise_sum(S.shift + S.ioff[it], S.K[p]);
+            S.st[p] = (tot <= S.tol || S.iter[p] >= a.max_iter) ? ST_FINAL : ST_RUN;
+          }
+        } else {
+          S.st[p] = ST_DONE;
+          S.inert[p] = static_cast<float>(S.iinert[it]);
+        }
+      }
+      __syncthreads();
+      // write back the centres (and norms) of problems that sweep again
+      for (int e = tid; e < ncols * DP; e += NT) {
+        const int sl = e / DP, d = e - sl * DP;
+        const int it = S.sitem[sl];
+        if (S.ikind[it] != IK_RUN) continue;
+        const int p = S.iprob[it];
+        if (S.st[p] == ST_DONE) continue;
+        cen[(S.cenoff[p] + (sl - S.ioff[it])) * DP + d] = Sm[e];
+      }
+      if (tid < ncols) {
+        const int it = S.sitem[tid];
+        if (S.ikind[it] == IK_RUN) {
+          const int p = S.iprob[it];
+          if (S.st[p] != ST_DONE) cenn[S.cenoff[p] + (tid - S.ioff[it])] = row_sq(Sm + tid * DP, a.dreal);
+        }
+      }
       __syncthreads();
     }
-    const int kidx = S.kidx[p0];
-    const uint8_t* lb = glab + static_cast<size_t>(best) * m;
-    uint8_t* out = a.labels_out + static_cast<size_t>(kidx) * a.n * a.ldl + h;
-    for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = lb[r];
-    if (tid == 0) {
-      if (a.inertia_out) a.inertia_out[static_cast<size_t>(kidx) * a.H + h] = S.inert[best];
-      if (a.niter_out) a.niter_out[static_cast<size_t>(kidx) * a.H + h] = S.iter[best];
+
+    // ---- best of n_init per K, output (KMeans.fit :1495-1531) -------------------
+    for (int p0 = 0; p0 < P; p0 += a.n_init) {
+      int best = p0;
+      for (int i = 1; i < a.n_init; ++i) {
+        const int p = p0 + i;
+        if (!(S.inert[p] < S.inert[best])) continue;
+        // _is_same_clustering(labels_p, labels_best): labels_p -> labels_best must be a function
+        if (tid <= KMAX) S.map[tid] = -1;
+        if (tid == 0) S.flag = 0;
+        __syncthreads();
+        const uint8_t* l1 = glab + static_cast<size_t>(p) * m;
+        const uint8_t* l2 = glab + static_cast<size_t>(best) * m;
+        for (int r = tid; r < m; r += NT) S.map[l1[r]] = l2[r];
+        __syncthreads();
+        bool bad = false;
+        for (int r = tid; r < m; r += NT) bad |= (S.map[l1[r]] != l2[r]);
+        if (bad) S.flag = 1;
+        __syncthreads();
+        if (S.flag) best = p;
+        __syncthreads();
+      }
+      const int kidx = S.kidx[p0];
+      const uint8_t* lb = glab + static_cast<size_t>(best) * m;
+      uint8_t* out = a.labels_out + static_cast<size_t>(kidx) * a.n * a.ldl + h;
+      for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = lb[r];
+      if (tid == 0) {
+        if (a.inertia_out) a.inertia_out[static_cast<size_t>(kidx) * a.H + h] = S.inert[best];
+        if (a.niter_out) a.niter_out[static_cast<size_t>(kidx) * a.H + h] = S.iter[best];
+      }
     }
   }
   if (tid == 0 && a.stats) {
@@ -986,30 +1039,55 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     atomicAdd(&a.stats[1], S.n_seed);
     atomicAdd(&a.stats[2], S.n_mrows);
     atomicAdd(&a.stats[3], S.n_reloc);
+    atomicAdd(&a.stats[4], S.n_sweeps);
+    atomicAdd(&a.stats[5], S.n_ctiles);
   }
+}
+
+// f16 hi/lo image of the rows: Xhl[r][0][d] = f16(x s), Xhl[r][1][d] = f16(x s - hi), s = 2^e.
+__global__ void split_kernel(const float* X, long long total, int dpad, float scale, uint16_t* Xhl) {
+  const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long long row = i / dpad;
+  const int d = static_cast<int>(i - row * dpad);
+  const float xs = X[i] * scale;
+  const _Float16 hi = static_cast<_Float16>(xs);
+  const _Float16 lo = static_cast<_Float16>(xs - static_cast<float>(hi));
+  Xhl[row * 2 * dpad + d] = __builtin_bit_cast(uint16_t, hi);
+  Xhl[row * 2 * dpad + dpad + d] = __builtin_bit_cast(uint16_t, lo);
 }
 
 int local_trials(int K) { return 2 + static_cast<int>(std::log(static_cast<double>(K))); }
 
 struct WsLayout {
-  int Pws = 0, Tws = 0, Kws = 0;
-  size_t off_dbuf = 0, off_cpos = 0, per_wg = 0;
+  int Pws = 0, Cws = 0, Kws = 0, Tws = 0;
+  size_t off_cen = 0, off_cenn = 0, off_cpos = 0, off_dbuf = 0, off_tsum = 0, off_rdist = 0, per_wg = 0;
 };
 
-WsLayout ws_layout(int m, const int32_t* groups, int nG) {
+constexpr size_t WS_HEADER = 256;  // the work counter
+
+WsLayout ws_layout(int m, int dpad, const int32_t* units, int nU, int seedmax) {
   WsLayout L;
-  for (int g = 0; g < nG; ++g) {
-    const int32_t* gd = groups + static_cast<size_t>(g) * GS;
+  for (int g = 0; g < nU; ++g) {
+    const int32_t* gd = units + static_cast<size_t>(g) * US;
     L.Pws = std::max(L.Pws, gd[0]);
+    int cols = 0;
     for (int p = 0; p < gd[0]; ++p) {
       L.Kws = std::max(L.Kws, gd[1 + 4 * p]);
       L.Tws = std::max(L.Tws, gd[4 + 4 * p]);
+      cols += gd[1 + 4 * p];
     }
+    L.Cws = std::max(L.Cws, cols);
   }
+  const int T = (m + RT - 1) / RT;
   auto al = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
-  L.off_dbuf = al(static_cast<size_t>(L.Pws) * m);
-  L.off_cpos = L.off_dbuf + al(static_cast<size_t>(L.Pws) * (L.Tws + 1) * m * sizeof(float));
-  L.per_wg = L.off_cpos + al(static_cast<size_t>(L.Pws) * L.Kws * sizeof(int32_t));
+  L.off_cen = al(static_cast<size_t>(L.Pws) * m);
+  L.off_cenn = L.off_cen + al(static_cast<size_t>(L.Cws) * dpad * sizeof(float));
+  L.off_cpos = L.off_cenn + al(static_cast<size_t>(L.Cws) * sizeof(float));
+  L.off_dbuf = L.off_cpos + al(static_cast<size_t>(L.Pws) * L.Kws * sizeof(int32_t));
+  L.off_tsum = L.off_dbuf + al(static_cast<size_t>(seedmax) * (L.Tws + 1) * m * sizeof(float));
+  L.off_rdist = L.off_tsum + al(static_cast<size_t>(seedmax) * L.Tws * T * sizeof(double));
+  L.per_wg = L.off_rdist + al(static_cast<size_t>(m) * sizeof(float));
   return L;
 }
 
@@ -1020,41 +1098,47 @@ void launch(const KArgs& a, unsigned blocks, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int cc_kmeans_plan(const int32_t* Ks, int nK, int n_init, int32_t* groups,
-                              int max_groups) {
-  if (!Ks || nK <= 0 || n_init <= 0 || !groups || max_groups <= 0) {
+extern "C" int cc_kmeans_plan(const int32_t* Ks, int nK, int n_init, int n_sub, int32_t* units,
+                              int max_units) {
+  if (!Ks || nK <= 0 || n_init <= 0 || n_sub <= 0 || !units || max_units <= 0) {
     cc::set_error("cc_kmeans_plan: bad arguments");
     return CC_ERR_ARG;
   }
+  if (n_init > PMAX) {
+    cc::set_error("cc_kmeans_plan: n_init must be <= 64");
+    return CC_ERR_UNSUPPORTED;
+  }
   std::vector<int> order(nK);
   for (int i = 0; i < nK; ++i) {
-    if (Ks[i] < 1 || Ks[i] > KMAX || Ks[i] * n_init > CMAX || n_init > PMAX) {
-      cc::set_error("cc_kmeans_plan: need 1 <= K <= 127 and K * n_init <= 128 (n_init <= 32)");
+    if (Ks[i] < 1 || Ks[i] > KMAX) {
+      cc::set_error("cc_kmeans_plan: need 1 <= K <= 127");
       return CC_ERR_UNSUPPORTED;
     }
     order[i] = i;
   }
-  // first-fit decreasing by K: heavy groups first (they also dispatch first)
+  // every unit must hold <= PMAX problems: at least ceil(nK*n_init / PMAX) units
+  const int per_unit = PMAX / n_init;  // K groups per unit
+  const int nU = std::max(n_sub, (nK + per_unit - 1) / per_unit);
+  if (nU > max_units) {
+    cc::set_error("cc_kmeans_plan: max_units too small");
+    return CC_ERR_ARG;
+  }
+  // largest K first (longest critical paths admitted first); greedy balance of K^2 cost
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return Ks[x] > Ks[y]; });
-  std::vector<int> cols, probs;
-  int nG = 0;
+  std::vector<double> cost(nU, 0.0);
+  std::vector<int> probs(nU, 0);
+  std::fill(units, units + static_cast<size_t>(nU) * US, 0);
   for (int k : order) {
-    const int need = Ks[k] * n_init;
-    int g = 0;
-    for (; g < nG; ++g)
-      if (cols[g] + need <= CMAX && probs[g] + n_init <= PMAX) break;
-    if (g == nG) {
-      if (nG == max_groups) {
-        cc::set_error("cc_kmeans_plan: max_groups too small");
-        return CC_ERR_ARG;
-      }
-      cols.push_back(0);
-      probs.push_back(0);
-      int32_t* gd = groups + static_cast<size_t>(nG) * GS;
-      std::fill(gd, gd + GS, 0);
-      ++nG;
+    int g = -1;
+    for (int u = 0; u < nU; ++u) {
+      if (probs[u] + n_init > PMAX) continue;
+      if (g < 0 || cost[u] < cost[g]) g = u;
     }
-    int32_t* gd = groups + static_cast<size_t>(g) * GS;
+    if (g < 0) {
+      cc::set_error("cc_kmeans_plan: internal packing failure");
+      return CC_ERR_ARG;
+    }
+    int32_t* gd = units + static_cast<size_t>(g) * US;
     for (int i = 0; i < n_init; ++i) {
       const int p = probs[g] + i;
       gd[1 + 4 * p] = Ks[k];
@@ -1063,28 +1147,55 @@ extern "C" int cc_kmeans_plan(const int32_t* Ks, int nK, int n_init, int32_t* gr
       gd[4 + 4 * p] = local_trials(Ks[k]);
     }
     probs[g] += n_init;
-    cols[g] += need;
     gd[0] = probs[g];
+    cost[g] += static_cast<double>(Ks[k]) * (Ks[k] + 8) * n_init;
   }
-  return nG;
+  // drop empty units (n_sub larger than the number of K groups)
+  int w = 0;
+  for (int u = 0; u < nU; ++u) {
+    if (units[static_cast<size_t>(u) * US] == 0) continue;
+    if (w != u) std::copy(units + static_cast<size_t>(u) * US, units + static_cast<size_t>(u + 1) * US,
+                          units + static_cast<size_t>(w) * US);
+    ++w;
+  }
+  return w;
 }
 
-extern "C" size_t cc_kmeans_workspace_bytes(int m, const int32_t* groups_host, int nG, int nh) {
-  if (m <= 0 || !groups_host || nG <= 0 || nh <= 0) return 0;
-  return ws_layout(m, groups_host, nG).per_wg * static_cast<size_t>(nG) * nh;
+extern "C" size_t cc_kmeans_workspace_bytes(int m, int dpad, const int32_t* units_host, int nU,
+                                            int seedmax, int grid) {
+  if (m <= 0 || !units_host || nU <= 0 || seedmax <= 0 || grid <= 0) return 0;
+  return WS_HEADER + ws_layout(m, dpad, units_host, nU, seedmax).per_wg * static_cast<size_t>(grid);
 }
 
-extern "C" int cc_kmeans_batched(const float* X, const float* xnorm, int n, int dreal, int dpad,
-                                 const int32_t* idx_hm, int H, int m, int h_begin, int h_end,
-                                 const int32_t* groups, const int32_t* groups_host, int nG,
-                                 int n_init, int max_iter, double tol_rel, const double* kpp_u,
-                                 int kpp_stride, const int32_t* kpp_pos, uint8_t* labels_nh,
-                                 int ldl, float* inertia, int32_t* n_iter,
-                                 unsigned long long* stats, void* workspace, size_t ws_bytes,
-                                 void* stream) {
-  if (!X || !xnorm || !idx_hm || !groups || !groups_host || !kpp_u || !kpp_pos || !labels_nh ||
-      n <= 0 || m <= 0 || m > n || H <= 0 || h_begin < 0 || h_end > H || h_end < h_begin ||
-      nG <= 0 || n_init <= 0 || max_iter <= 0 || dreal <= 0 || dreal > dpad || ldl < H) {
+extern "C" int cc_split_f16(const float* X, int n, int dpad, int scale_exp, uint16_t* Xhl, void* stream) {
+  if (!X || !Xhl || n <= 0 || dpad <= 0 || scale_exp < -62 || scale_exp > 62) {
+    cc::set_error("cc_split_f16: bad arguments");
+    return CC_ERR_ARG;
+  }
+  const long long total = static_cast<long long>(n) * dpad;
+  const unsigned blocks = static_cast<unsigned>((total + 255) / 256);
+  hipLaunchKernelGGL(split_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), X, total,
+                     dpad, std::ldexp(1.0f, scale_exp), Xhl);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cc::set_error(std::string("cc_split_f16: ") + hipGetErrorString(e));
+    return CC_ERR_HIP;
+  }
+  return CC_OK;
+}
+
+extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const float* xnorm, int n,
+                                 int dreal, int dpad, int scale_exp, const int32_t* idx_hm, int H,
+                                 int m, int h_begin, int h_end, const int32_t* units,
+                                 const int32_t* units_host, int nU, int n_init, int max_iter,
+                                 double tol_rel, const double* kpp_u, int kpp_stride,
+                                 const int32_t* kpp_pos, uint8_t* labels_nh, int ldl, float* inertia,
+                                 int32_t* n_iter, unsigned long long* stats, void* workspace,
+                                 size_t ws_bytes, int grid, int seedmax, void* stream) {
+  if (!X || !Xhl || !xnorm || !idx_hm || !units || !units_host || !kpp_u || !kpp_pos || !labels_nh ||
+      n <= 0 || m <= 0 || m > n || H <= 0 || h_begin < 0 || h_end > H || h_end < h_begin || nU <= 0 ||
+      n_init <= 0 || max_iter <= 0 || dreal <= 0 || dreal > dpad || ldl < H || grid <= 0 ||
+      seedmax <= 0 || seedmax > 32 || scale_exp < -62 || scale_exp > 62) {
     cc::set_error("cc_kmeans_batched: bad arguments");
     return CC_ERR_ARG;
   }
@@ -1093,26 +1204,21 @@ extern "C" int cc_kmeans_batched(const float* X, const float* xnorm, int n, int 
     return CC_ERR_UNSUPPORTED;
   }
   int kmax = 0, tmax = 0;
-  for (int g = 0; g < nG; ++g) {
-    const int32_t* gd = groups_host + static_cast<size_t>(g) * GS;
-    int cols = 0;
+  for (int g = 0; g < nU; ++g) {
+    const int32_t* gd = units_host + static_cast<size_t>(g) * US;
     if (gd[0] <= 0 || gd[0] > PMAX || gd[0] % n_init != 0) {
-      cc::set_error("cc_kmeans_batched: malformed group descriptor");
+      cc::set_error("cc_kmeans_batched: malformed unit descriptor");
       return CC_ERR_ARG;
     }
     for (int p = 0; p < gd[0]; ++p) {
       const int K = gd[1 + 4 * p];
-      if (K < 1 || K > KMAX || K > m || gd[4 + 4 * p] != local_trials(K) || gd[4 + 4 * p] > TMAX) {
-        cc::set_error("cc_kmeans_batched: bad K in group (1 <= K <= min(127, m))");
+      if (K < 1 || K > KMAX || K > m || gd[4 + 4 * p] != local_trials(K) || gd[4 + 4 * p] > TMAX ||
+          gd[3 + 4 * p] < 0 || gd[3 + 4 * p] >= n_init || gd[2 + 4 * p] < 0 || gd[2 + 4 * p] > 255) {
+        cc::set_error("cc_kmeans_batched: bad problem in unit (1 <= K <= min(127, m))");
         return CC_ERR_ARG;
       }
-      cols += K;
       kmax = std::max(kmax, K);
       tmax = std::max(tmax, gd[4 + 4 * p]);
-    }
-    if (cols > CMAX) {
-      cc::set_error("cc_kmeans_batched: group exceeds 128 centroid columns");
-      return CC_ERR_ARG;
     }
   }
   if (kpp_stride < 1 + (kmax - 1) * tmax) {
@@ -1121,27 +1227,32 @@ extern "C" int cc_kmeans_batched(const float* X, const float* xnorm, int n, int 
   }
   const int nh = h_end - h_begin;
   if (nh == 0) return CC_OK;
-  const WsLayout L = ws_layout(m, groups_host, nG);
-  if (!workspace || ws_bytes < L.per_wg * static_cast<size_t>(nG) * nh) {
+  const WsLayout L = ws_layout(m, dpad, units_host, nU, seedmax);
+  if (!workspace || ws_bytes < WS_HEADER + L.per_wg * static_cast<size_t>(grid)) {
     cc::set_error("cc_kmeans_batched: workspace too small");
     return CC_ERR_ARG;
   }
-  const size_t blocks = static_cast<size_t>(nG) * nh;
-  if (blocks > 0x7fffffffu) {
-    cc::set_error("cc_kmeans_batched: too many workgroups");
-    return CC_ERR_ARG;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(workspace, 0, sizeof(unsigned), st);
+  if (e != hipSuccess) {
+    cc::set_error(std::string("cc_kmeans_batched: ") + hipGetErrorString(e));
+    return CC_ERR_HIP;
   }
   KArgs a{};
   a.X = X;
+  a.Xhl = Xhl;
   a.xnorm = xnorm;
-  a.ldx = dpad;
   a.dreal = dreal;
+  a.scale = std::ldexp(1.0f, scale_exp);
+  a.inv_scale = std::ldexp(1.0f, -scale_exp);
+  a.dscale = std::ldexp(1.0f, 1 - 2 * scale_exp);
   a.idx = idx_hm;
   a.m = m;
   a.h_begin = h_begin;
   a.nh = nh;
-  a.groups = groups;
-  a.nG = nG;
+  a.T = (m + RT - 1) / RT;
+  a.units = units;
+  a.nU = nU;
   a.max_iter = max_iter;
   a.tol_rel = tol_rel;
   a.kpp_u = kpp_u;
@@ -1155,20 +1266,26 @@ extern "C" int cc_kmeans_batched(const float* X, const float* xnorm, int n, int 
   a.inertia_out = inertia;
   a.niter_out = n_iter;
   a.stats = stats;
-  a.ws = static_cast<uint8_t*>(workspace);
+  a.counter = static_cast<unsigned*>(workspace);
+  a.ws = static_cast<uint8_t*>(workspace) + WS_HEADER;
   a.ws_per_wg = L.per_wg;
-  a.off_dbuf = L.off_dbuf;
+  a.off_cen = L.off_cen;
+  a.off_cenn = L.off_cenn;
   a.off_cpos = L.off_cpos;
+  a.off_dbuf = L.off_dbuf;
+  a.off_tsum = L.off_tsum;
+  a.off_rdist = L.off_rdist;
   a.Pws = L.Pws;
-  a.Tws = L.Tws;
   a.Kws = L.Kws;
-  const hipStream_t st = static_cast<hipStream_t>(stream);
+  a.Tws = L.Tws;
+  a.seedmax = seedmax;
+  const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nU));
   switch (dpad) {
-    case 32: launch<32>(a, static_cast<unsigned>(blocks), st); break;
-    case 64: launch<64>(a, static_cast<unsigned>(blocks), st); break;
-    default: launch<128>(a, static_cast<unsigned>(blocks), st); break;
+    case 32: launch<32>(a, blocks, st); break;
+    case 64: launch<64>(a, blocks, st); break;
+    default: launch<128>(a, blocks, st); break;
   }
-  hipError_t e = hipGetLastError();
+  e = hipGetLastError();
   if (e != hipSuccess) {
     cc::set_error(std::string("cc_kmeans_batched: ") + hipGetErrorString(e));
     return CC_ERR_HIP;

@@ -19,7 +19,7 @@ import torch
 
 from . import _lib, engine
 
-GSTRIDE = 1 + 4 * 32
+USTRIDE = 1 + 4 * 64   # CC_KM_USTRIDE
 DPADS = (32, 64, 128)
 
 
@@ -27,14 +27,31 @@ def local_trials(K: int) -> int:
     return 2 + int(np.log(K))
 
 
-def plan(Ks, n_init: int) -> np.ndarray:
-    """int32 [nG, GSTRIDE] group descriptors (see include/ccmi.h)."""
+def plan(Ks, n_init: int, n_sub: int = 1) -> np.ndarray:
+    """int32 [nU, USTRIDE] unit descriptors (see include/ccmi.h)."""
     Ks = np.ascontiguousarray(np.asarray(Ks, dtype=np.int32))
-    buf = np.zeros((len(Ks) + 1, GSTRIDE), dtype=np.int32)
-    nG = _lib.load().cc_kmeans_plan(Ks.ctypes.data, len(Ks), int(n_init), buf.ctypes.data, buf.shape[0])
-    if nG <= 0:
-        _lib.check(nG, "cc_kmeans_plan")
-    return buf[:nG].copy()
+    cap = max(int(n_sub), len(Ks)) + 1
+    buf = np.zeros((cap, USTRIDE), dtype=np.int32)
+    nU = _lib.load().cc_kmeans_plan(Ks.ctypes.data, len(Ks), int(n_init), int(n_sub),
+                                    buf.ctypes.data, cap)
+    if nU <= 0:
+        _lib.check(nU, "cc_kmeans_plan")
+    return buf[:nU].copy()
+
+
+def choose_subsets(nh: int, n_groups: int, cus: int) -> int:
+    """Units per resample: enough units to fill every CU of the persistent grid with a
+    balanced last round, as few as possible (bigger units pack their sweeps better)."""
+    best, best_eff = 1, -1.0
+    for s in range(1, max(1, n_groups) + 1):
+        units = nh * s
+        rounds = -(-units // cus)
+        eff = units / (cus * rounds) if units >= cus else units / cus
+        if eff >= 0.85:
+            return s
+        if eff > best_eff + 1e-9:
+            best, best_eff = s, eff
+    return best
 
 
 def kpp_tables(Ks, n_init: int, seed: int, m: int, weight_dtype=np.float32):
@@ -59,12 +76,22 @@ def kpp_tables(Ks, n_init: int, seed: int, m: int, weight_dtype=np.float32):
     return u, pos, stride
 
 
+def scale_exponent(amax: float) -> int:
+    """e with max|X| * 2^e <= 2^14, so the f16 hi/lo operand pair stays in range."""
+    if not np.isfinite(amax):
+        raise ValueError("X contains non-finite values")
+    if amax == 0.0:
+        return 0
+    return int(np.clip(14 - int(np.ceil(np.log2(amax))), -62, 62))
+
+
 def prepare_rows(X, device):
-    """Mean-centred float32 rows zero-padded to dpad, and their squared norms, on device.
+    """Mean-centred float32 rows zero-padded to dpad, their squared norms, and the f16 hi/lo
+    MFMA operand image of the rows (cc_split_f16), on device.
 
     X is a host array or a device tensor (already resident in HBM).  sklearn centres
     X_sub by its own mean (_kmeans.py:1479-1481); distances are translation invariant,
-    so one global centring serves every resample.
+    so one global centring serves every resample.  Returns (Xd, xnorm, dpad, Xhl, e).
     """
     n, d = X.shape
     dpad = next((p for p in DPADS if d <= p), None)
@@ -76,48 +103,62 @@ def prepare_rows(X, device):
     Xd = torch.zeros((n, dpad), dtype=torch.float32, device=device)
     Xd[:, :d] = Xt.to(torch.float32) - mean
     xnorm = (Xd * Xd).sum(dim=1).contiguous()
-    return Xd, xnorm, dpad
+    e = scale_exponent(float(Xd.abs().max().item()) if n else 0.0)
+    Xhl = torch.empty((n, 2, dpad), dtype=torch.int16, device=device)
+    _lib.call("cc_split_f16", Xd.data_ptr(), n, dpad, e, Xhl.data_ptr(), engine.stream_ptr(device))
+    return Xd, xnorm, dpad, Xhl, e
 
 
 class BatchedKMeans:
     """All (h, K, init) k-means problems of a consensus fit, on one device."""
 
     def __init__(self, Ks, n_init=3, max_iter=300, tol=1e-4, random_state=0,
-                 workspace_budget=8 << 30):
+                 workspace_budget=8 << 30, seedmax=16):
         self.Ks = [int(k) for k in Ks]
         self.n_init = int(n_init)
         self.max_iter = int(max_iter)
         self.tol = float(tol)
         self.seed = int(random_state)
         self.workspace_budget = int(workspace_budget)
-        self.groups = plan(self.Ks, self.n_init)
+        self.seedmax = int(seedmax)
         self.stats = None
+        self.units = None
 
     def run(self, Xd, xnorm, dreal, idx_d, n, H, m, h_begin, h_end, labels_nh, weight_dtype,
-            inertia=None, n_iter=None):
+            inertia=None, n_iter=None, Xhl=None, scale_exp=None):
         """Fill labels_nh[k, :, h] for h in [h_begin, h_end) (uint8 [nK, n, ldl])."""
         dev = Xd.device
         if max(self.Ks) > m:
             raise ValueError(f"n_samples={m} should be >= n_clusters={max(self.Ks)}.")
+        if Xhl is None:
+            raise _lib.CCMIError("BatchedKMeans.run needs the f16 operand image (prepare_rows)")
+        nh = h_end - h_begin
+        self.stats = torch.zeros(8, dtype=torch.int64, device=dev)
+        if nh <= 0:
+            return labels_nh
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        n_sub = choose_subsets(nh, len(self.Ks), cus)
+        u_h = plan(self.Ks, self.n_init, n_sub)
+        self.units = u_h
+        nU = u_h.shape[0]
+        seedmax = max(1, min(self.seedmax, 32, int(u_h[:, 0].max())))
         u, pos, stride = kpp_tables(self.Ks, self.n_init, self.seed, m, weight_dtype)
         u_d = torch.from_numpy(u).to(dev)
         pos_d = torch.from_numpy(pos).to(dev)
-        g_h = np.ascontiguousarray(self.groups)
-        g_d = torch.from_numpy(g_h).to(dev)
-        nG = g_h.shape[0]
+        u_d_units = torch.from_numpy(u_h).to(dev)
         lib = _lib.load()
-        per_h = lib.cc_kmeans_workspace_bytes(m, g_h.ctypes.data, nG, 1)
-        hb = max(1, min(h_end - h_begin, self.workspace_budget // max(per_h, 1)))
-        ws = torch.empty(per_h * hb, dtype=torch.uint8, device=dev)
-        self.stats = torch.zeros(64, dtype=torch.int64, device=dev)  # [0:4] counters, rest: diagnostics
+        per = lambda g: lib.cc_kmeans_workspace_bytes(m, Xd.shape[1], u_h.ctypes.data, nU, seedmax, g)
+        grid = min(cus, nh * nU)
+        while grid > 1 and per(grid) > self.workspace_budget:
+            grid //= 2
+        ws = torch.empty(per(grid), dtype=torch.uint8, device=dev)
         ldl = labels_nh.stride(1)
-        for h0 in range(h_begin, h_end, hb):
-            h1 = min(h_end, h0 + hb)
-            with engine.timed("cc_kmeans_batched"):
-                _lib.call("cc_kmeans_batched", Xd.data_ptr(), xnorm.data_ptr(), n, int(dreal),
-                          Xd.shape[1], idx_d.data_ptr(), H, m, h0, h1, g_d.data_ptr(),
-                          g_h.ctypes.data, nG, self.n_init, self.max_iter, self.tol,
-                          u_d.data_ptr(), stride, pos_d.data_ptr(), labels_nh.data_ptr(), ldl,
-                          _lib.ptr(inertia), _lib.ptr(n_iter), self.stats.data_ptr(),
-                          ws.data_ptr(), ws.numel(), engine.stream_ptr(dev))
+        with engine.timed("cc_kmeans_batched"):
+            _lib.call("cc_kmeans_batched", Xd.data_ptr(), Xhl.data_ptr(), xnorm.data_ptr(), n,
+                      int(dreal), Xd.shape[1], int(scale_exp), idx_d.data_ptr(), H, m, h_begin,
+                      h_end, u_d_units.data_ptr(), u_h.ctypes.data, nU, self.n_init,
+                      self.max_iter, self.tol, u_d.data_ptr(), stride, pos_d.data_ptr(),
+                      labels_nh.data_ptr(), ldl, _lib.ptr(inertia), _lib.ptr(n_iter),
+                      self.stats.data_ptr(), ws.data_ptr(), ws.numel(), grid, seedmax,
+                      engine.stream_ptr(dev))
         return labels_nh

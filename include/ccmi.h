@@ -16,7 +16,8 @@
  *   cc_cosample           CC.py:264  I = S^T S            (int8 MFMA, upper-triangle tiles)
  *   cc_coassoc            CC.py:287-290 + :338-344  M += L^T L fused with the 20-bin histogram
  *   cc_consensus          CC.py:372-373  C = f32(M) / f32(I + 1e-6), diag 1
- *   cc_kmeans_plan        packing of the (K, init) problems of one resample into workgroups
+ *   cc_kmeans_plan        packing of the (K, init) problems of one resample into units
+ *   cc_split_f16          f16 hi/lo operand image of the rows for the k-means MFMAs
  *   cc_kmeans_batched     CC.py:282 clusterer.fit_predict for every (h, K) at once
  *                         (sklearn KMeans: k-means++ init, Lloyd, best of n_init)
  */
@@ -93,42 +94,54 @@ int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stre
  * and tol convergence, empty-cluster relocation, best of n_init;
  * sklearn/cluster/_kmeans.py:174-262, :624-752, :1427-1556).
  *
- * Problems are packed into GROUPS (cc_kmeans_plan): every (K, init) of a group shares
- * one resample's rows, so one workgroup runs a whole group for one resample and reads
- * each row once per sweep for all of the group's centroids (<= CC_KM_CMAX columns).
- * Group descriptor g (int32, CC_KM_GSTRIDE entries): [0] = P, then per problem p:
- * [1+4p] = K, [2+4p] = kidx (index into Ks), [3+4p] = init, [4+4p] = local trials. */
-#define CC_KM_PMAX 32
-#define CC_KM_CMAX 128
-#define CC_KM_GSTRIDE (1 + 4 * CC_KM_PMAX)
+ * Work is split into UNITS = (resample, subset of the (K, init) problems); a persistent
+ * grid of workgroups pulls units from an atomic counter and runs each unit's fits as one
+ * problem engine (every sweep streams the resample's rows once for up to 256 centroid
+ * slots, packed round-robin from the unit's seeding and Lloyd problems).
+ * Unit descriptor u (int32, CC_KM_USTRIDE entries): [0] = P (<= CC_KM_PMAX, the n_init
+ * runs of one K consecutive), then per problem p: [1+4p] = K, [2+4p] = kidx (index into
+ * Ks), [3+4p] = init, [4+4p] = local trials. */
+#define CC_KM_PMAX 64
+#define CC_KM_USTRIDE (1 + 4 * CC_KM_PMAX)
 
-/* Pack the (K, n_init) units of Ks[0..nK) into groups; returns the group count (> 0) or a
- * negative error.  groups must hold max_groups * CC_KM_GSTRIDE int32. */
-int cc_kmeans_plan(const int32_t* Ks, int nK, int n_init, int32_t* groups, int max_groups);
+/* Pack the (K, n_init) groups of Ks[0..nK) into at least n_sub units (balanced by a K^2
+ * cost proxy, largest K first); returns the unit count (> 0) or a negative error.
+ * units must hold max_units * CC_KM_USTRIDE int32. */
+int cc_kmeans_plan(const int32_t* Ks, int nK, int n_init, int n_sub, int32_t* units, int max_units);
 
-/* Workspace bytes for one cc_kmeans_batched launch over nh resamples. */
-size_t cc_kmeans_workspace_bytes(int m, const int32_t* groups_host, int nG, int nh);
+/* Workspace bytes of a cc_kmeans_batched launch with `grid` workgroups. */
+size_t cc_kmeans_workspace_bytes(int m, int dpad, const int32_t* units_host, int nU, int seedmax,
+                                 int grid);
+
+/* f16 hi/lo image of the rows for the MFMA operands: Xhl[r][0][d] = f16(X[r][d] * 2^e),
+ * Xhl[r][1][d] = f16(X[r][d] * 2^e - hi), e in [-62, 62] (host-chosen so that
+ * max|X| * 2^e <= 2^14).  X [n][dpad] f32, Xhl [n][2][dpad] uint16. */
+int cc_split_f16(const float* X, int n, int dpad, int scale_exp, uint16_t* Xhl, void* stream);
 
 /*  X         [n][dpad] float32, mean-centred, zero-padded from dreal to dpad in {32,64,128}
+ *  Xhl       cc_split_f16 image of X with the same scale_exp
  *  xnorm     [n] float32 squared row norms of X
  *  idx_hm    [H][m] int32 resample rows; this launch runs resamples [h_begin, h_end)
- *  groups    device copy of the plan; groups_host the same array on the host
+ *  units     device copy of the plan; units_host the same array on the host
  *  kpp_u     [nK][n_init][kpp_stride] float64: the RandomState(seed) doubles of each
  *            (K, init) k-means++ run (entry 0: the first-centre draw, consumed on the host)
  *  kpp_pos   [nK][n_init] int32 first-centre positions in resample order
  *  labels_nh [nK][n][ldl] uint8 output (pre-filled 0xFF); labels_nh[k][idx[h][r]][h]
  *  inertia   optional [nK][H] float32; n_iter optional [nK][H] int32
- *  stats     optional [4] uint64 accumulated: {Lloyd row x centroid distance products,
+ *  stats     optional [8] uint64 accumulated: {Lloyd row x centroid distance products,
  *            seeding row x candidate distance products, Lloyd M-step row updates
- *            (rows x running problems), empty-cluster relocations}
- *  All device pointers except groups_host. */
-int cc_kmeans_batched(const float* X, const float* xnorm, int n, int dreal, int dpad,
-                      const int32_t* idx_hm, int H, int m, int h_begin, int h_end,
-                      const int32_t* groups, const int32_t* groups_host, int nG, int n_init,
-                      int max_iter, double tol_rel, const double* kpp_u, int kpp_stride,
-                      const int32_t* kpp_pos, uint8_t* labels_nh, int ldl, float* inertia,
-                      int32_t* n_iter, unsigned long long* stats, void* workspace,
-                      size_t ws_bytes, void* stream);
+ *            (rows x running problems), empty-cluster relocations, sweeps,
+ *            32-slot column tiles x row tiles swept}
+ *  grid      workgroups (<= units; one per CU is the intended size)
+ *  seedmax   problems of a unit seeding concurrently (1..32)
+ *  All pointers except units_host are device pointers. */
+int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const float* xnorm, int n, int dreal,
+                      int dpad, int scale_exp, const int32_t* idx_hm, int H, int m, int h_begin,
+                      int h_end, const int32_t* units, const int32_t* units_host, int nU,
+                      int n_init, int max_iter, double tol_rel, const double* kpp_u,
+                      int kpp_stride, const int32_t* kpp_pos, uint8_t* labels_nh, int ldl,
+                      float* inertia, int32_t* n_iter, unsigned long long* stats,
+                      void* workspace, size_t ws_bytes, int grid, int seedmax, void* stream);
 
 #ifdef __cplusplus
 }

@@ -31,12 +31,13 @@ def run_gpu(X, Ks, H, frac, seed, n_init=3):
     m = int(frac * n)
     idx = engine.resample_indices(seed, n, m, 0, H)
     idx_d = torch.from_numpy(idx).to(dev)
-    Xd, xn, _ = prepare_rows(X, dev)
+    Xd, xn, _, Xhl, e = prepare_rows(X, dev)
     L = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
     inert = torch.zeros((len(Ks), H), dtype=torch.float32, device=dev)
     nit = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
     bk = BatchedKMeans(Ks, n_init=n_init, random_state=seed)
-    bk.run(Xd, xn, d, idx_d, n, H, m, 0, H, L, np.float32, inertia=inert, n_iter=nit)
+    bk.run(Xd, xn, d, idx_d, n, H, m, 0, H, L, np.float32, inertia=inert, n_iter=nit, Xhl=Xhl,
+           scale_exp=e)
     torch.cuda.synchronize()
     Lh = L.cpu().numpy()
     labs = np.stack([np.stack([Lh[k][idx[h], h] for h in range(H)]) for k in range(len(Ks))])
@@ -86,19 +87,21 @@ def test_every_sampled_row_labelled_once():
 
 
 def test_launch_split_is_invariant():
-    """Resample batching over several launches (and hence over GPUs) changes nothing."""
+    """Resample batching over several launches (and hence over GPUs), the persistent grid size
+    and the unit split change nothing."""
     dev = engine.require_gpu()
     X = blobs(800, 20, 4, seed=3)
     n, d = X.shape
     Ks, H, m = [2, 4, 6], 12, 640
     idx = engine.resample_indices(11, n, m, 0, H)
     idx_d = torch.from_numpy(idx).to(dev)
-    Xd, xn, _ = prepare_rows(X, dev)
+    Xd, xn, _, Xhl, e = prepare_rows(X, dev)
     L1 = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
     L2 = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
-    BatchedKMeans(Ks, random_state=11).run(Xd, xn, d, idx_d, n, H, m, 0, H, L1, np.float32)
-    bk = BatchedKMeans(Ks, random_state=11, workspace_budget=1)  # one resample per launch
-    bk.run(Xd, xn, d, idx_d, n, H, m, 0, 5, L2, np.float32)
-    bk.run(Xd, xn, d, idx_d, n, H, m, 5, H, L2, np.float32)
+    kw = dict(Xhl=Xhl, scale_exp=e)
+    BatchedKMeans(Ks, random_state=11).run(Xd, xn, d, idx_d, n, H, m, 0, H, L1, np.float32, **kw)
+    bk = BatchedKMeans(Ks, random_state=11, workspace_budget=1)  # one workgroup per launch
+    bk.run(Xd, xn, d, idx_d, n, H, m, 0, 5, L2, np.float32, **kw)
+    bk.run(Xd, xn, d, idx_d, n, H, m, 5, H, L2, np.float32, **kw)
     torch.cuda.synchronize()
     assert torch.equal(L1, L2)

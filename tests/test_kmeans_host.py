@@ -27,28 +27,48 @@ def test_kpp_stream_matches_sklearn(K, m, seed, dtype):
         np.testing.assert_array_equal(u[0, i, 1:L], raw[i * L + 1:(i + 1) * L])
 
 
-def test_plan_covers_every_problem_once():
+@pytest.mark.parametrize("n_sub", [1, 2, 5, 40])
+def test_plan_covers_every_problem_once(n_sub):
     Ks = list(range(2, 21))
-    g = kmeans.plan(Ks, 3)
+    g = kmeans.plan(Ks, 3, n_sub)
+    assert len(g) == min(max(n_sub, 1), len(Ks))
     seen = []
     for row in g:
         P = row[0]
-        assert P % 3 == 0 and P <= 32
-        cols = 0
+        assert P % 3 == 0 and 0 < P <= 64
         for p in range(P):
             K, kidx, init, ntr = row[1 + 4 * p: 5 + 4 * p]
             assert Ks[kidx] == K and ntr == kmeans.local_trials(K)
             assert init == p % 3
             seen.append((kidx, init))
-            cols += K
-        assert cols <= 128
+        # largest K first inside a unit (longest critical paths admitted first)
+        ks = [row[1 + 4 * p] for p in range(P)]
+        assert ks == sorted(ks, reverse=True)
     assert sorted(seen) == [(k, i) for k in range(len(Ks)) for i in range(3)]
-    # heavy groups first
-    assert g[0, 1] == 20
+
+
+def test_plan_splits_beyond_unit_capacity():
+    Ks = list(range(2, 40))  # 38 K x 3 inits = 114 problems > 64 per unit
+    g = kmeans.plan(Ks, 3, 1)
+    assert len(g) == 2 and g[:, 0].sum() == 114
 
 
 def test_plan_rejects_unsupported():
     from consensus_clustering_amd import _lib
 
     with pytest.raises(_lib.CCMIError):
-        kmeans.plan([64], 3)  # 192 columns > 128
+        kmeans.plan([128], 3)  # K > 127 (uint8 labels, 0xFF = not sampled)
+
+
+def test_choose_subsets_fills_the_grid():
+    assert kmeans.choose_subsets(1000, 19, 256) == 1
+    s = kmeans.choose_subsets(125, 19, 256)  # 8 GPUs at C3: 125 resamples per GPU
+    assert 125 * s >= 0.85 * 256
+    assert kmeans.choose_subsets(4, 3, 256) == 3
+
+
+def test_scale_exponent():
+    assert kmeans.scale_exponent(0.0) == 0
+    for amax in (1e-3, 0.7, 1.0, 3.0, 1e4, 6e4):
+        e = kmeans.scale_exponent(amax)
+        assert amax * 2.0 ** e <= 2 ** 14 and amax * 2.0 ** (e + 1) > 2 ** 14
