@@ -63,7 +63,7 @@ constexpr int NT = 512;
 constexpr int NW = 8;
 constexpr int RT = 32;              // rows per tile (one MFMA row block)
 constexpr int CW = 256;             // centroid slots per sweep (8 waves x 32)
-constexpr int NS = 8;               // E-step work items per thread (16 item lanes x 8)
+constexpr int NS = 4;               // E-step work items per thread (16 item lanes x 8)
 constexpr int IMAX = 16 * NS;       // work items per sweep
 constexpr int PMAX = CC_KM_PMAX;    // problems per unit
 constexpr int TMAX = 6;             // max local trials: 2 + floor(ln 127)
@@ -71,6 +71,20 @@ constexpr int KMAX = 127;
 constexpr int DSD = CW + 1;         // distance-tile row stride (floats): conflict-free b32 reads
 constexpr int NRING = 4;            // X tile ring: t+1 (gather), t (dist), t-2 (M-step)
 constexpr int US = CC_KM_USTRIDE;
+
+// Diagnostic build only (-DCC_KM_STAMPS): per-wave cycle accounting of the sweep phases of
+// workgroup 0, added into stats[8 + 8 * wave + k] (k: issue, dist, estep, mstep, commit,
+// barrier) and stats[72..75] (sweep prologue, post-processing, unit setup, output).
+#ifdef CC_KM_STAMPS
+#define KM_STAMP(var)                  \
+  __builtin_amdgcn_sched_barrier(0);   \
+  const unsigned long long var = __builtin_amdgcn_s_memtime(); \
+  __builtin_amdgcn_sched_barrier(0)
+#define KM_ACC(k, a, b) st_acc[k] += (b) - (a)
+#else
+#define KM_STAMP(var)
+#define KM_ACC(k, a, b)
+#endif
 
 enum { ST_WAIT = 0, ST_SEED = 1, ST_RUN = 2, ST_FINAL = 3, ST_DONE = 4 };
 enum { IK_SEED0 = 0, IK_SEED = 1, IK_RUN = 2, IK_FINAL = 3 };
@@ -99,6 +113,7 @@ struct KArgs {
   uint8_t* ws;
   size_t ws_per_wg, off_cen, off_cenn, off_cpos, off_dbuf, off_tsum, off_rdist;
   int Pws, Kws, Tws, seedmax;
+  int lsm;  // glab row stride (m rounded up to 64)
 };
 
 struct State {
@@ -142,8 +157,8 @@ struct Lay {
   static constexpr int S_BYTES = CW * DP * 4;  // centre sums [CW][DP] f32, aliasing ring + D
   static_assert(S_BYTES <= U_END, "centre sums must fit in the ring + distance tiles");
   static constexpr int OFF_LS = (U_END + 15) / 16 * 16;  // labels [2][IMAX][RT] u8
-  static constexpr int OFF_XN = OFF_LS + 2 * IMAX * RT;  // row norms [NRING][RT] f32
-  static constexpr int OFF_ST = OFF_XN + NRING * RT * 4;
+  static constexpr int OFF_XN = OFF_LS + 2 * IMAX * RT;  // row norms [NRING][64] f32 (DMA'd, 32 used)
+  static constexpr int OFF_ST = OFF_XN + NRING * 64 * 4;
   static constexpr int TOTAL = OFF_ST + ((sizeof(State) + 15) / 16) * 16;
   static_assert(TOTAL <= 163840, "LDS budget");
 };
@@ -196,55 +211,86 @@ __device__ __forceinline__ float row_sq(const float* c, int dreal) {
   return s;
 }
 
-// ---- X tile gather (all threads): issue the global loads early, commit to LDS late ----
+// XOR value of the swizzle of xoff<DP> for a row (chunk position = ch ^ xsw(row)).
 template <int DP>
-struct TileRegs {
-  static constexpr int CPR = DP / 4;            // 16-B chunks per row (hi + lo)
-  static constexpr int NCH = RT * CPR;
-  static constexpr int PER = (NCH + NT - 1) / NT;
-  u32x4 v[PER];
-  float xn;
+__device__ __forceinline__ int xsw(int row) {
+  if constexpr (DP == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else if constexpr (DP == 64) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+  else return (row >> 2) & 3;
+}
+
+// ---- X tile gather by LDS-DMA (global_load_lds_dwordx4: lane i of a wave-instruction writes
+// 16 B at M0 + 16 i, so one instruction fills a contiguous 1-KiB piece = 1024/(2 DP) whole rows
+// of the swizzled image; each lane fetches the chunk that lives at its linear position).
+// The data never passes through VGPRs; rows past m load the clamped row m-1 (consumers ignore
+// them: E-step rows are masked, their labels are 0xFF so the M-step one-hot is 0).
+template <int DP>
+struct Gather {
+  static constexpr int IMG = RT * DP * 2;
+  static constexpr int NI = (2 * IMG) / 1024;          // pieces per tile (hi + lo)
+  static constexpr int PER = (NI + NW - 1) / NW;       // pieces per wave
+  static constexpr int ROWB = 2 * DP;                  // bytes per image row
 };
 
 template <int DP>
-__device__ __forceinline__ void tile_issue(const KArgs& a, const int32_t* idx, int r0, int tid,
-                                           TileRegs<DP>& R) {
-  using TR = TileRegs<DP>;
-  int src[TR::PER];
+struct TileIdx {
+  int src[Gather<DP>::PER];
+  int xsrc;
+};
+
+template <int DP>
+__device__ __forceinline__ void idx_issue(const KArgs& a, const int32_t* idx, int r0, int wave, int lane,
+                                          TileIdx<DP>& I) {
+  using GA = Gather<DP>;
 #pragma unroll
-  for (int i = 0; i < TR::PER; ++i) {
-    const int e = tid + NT * i;
-    src[i] = idx[min(r0 + min(e / TR::CPR, RT - 1), a.m - 1)];
+  for (int j = 0; j < GA::PER; ++j) {
+    const int k = wave + NW * j;
+    const int B = 1024 * k + 16 * lane;
+    const int off = B % GA::IMG;
+    I.src[j] = idx[min(r0 + off / GA::ROWB, a.m - 1)];
   }
-  const int xr = min(r0 + (tid & (RT - 1)), a.m - 1);
-  const float xn = a.xnorm[idx[xr]];
-#pragma unroll
-  for (int i = 0; i < TR::PER; ++i) {
-    const int e = tid + NT * i;
-    const int row = e / TR::CPR, c = e - (e / TR::CPR) * TR::CPR;
-    const bool ok = e < TR::NCH && r0 + row < a.m;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (e < TR::NCH) v = *reinterpret_cast<const u32x4*>(a.Xhl + static_cast<size_t>(src[i]) * (2 * DP) + 8 * c);
-    R.v[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};
-  }
-  R.xn = (r0 + (tid & (RT - 1)) < a.m) ? xn : 0.f;
+  I.xsrc = idx[min(r0 + lane, a.m - 1)];
+}
+
+// LDS-DMA piece issued from inline asm: opaque to the compiler's waitcnt pass, which would
+// otherwise put a vmcnt(0) in front of every LDS read it cannot prove disjoint from the DMA
+// (the ds_read_b64_tr_b16 of the M-step), exposing the gather latency mid-iteration.
+// Untracked VMEM ops only make the compiler's own vmcnt waits stricter (the counter drains in
+// order); completion is awaited explicitly by dma_wait() before the barrier that publishes the
+// tile.  M0 is set inside the asm; no compiler-generated code in this kernel uses M0.
+__device__ __forceinline__ void dma_piece(const void* g, const void* lds_dst, int bytes) {
+  const unsigned la = static_cast<unsigned>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) const char*)lds_dst));
+  if (bytes == 16)
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g) : "memory");
 }
 
 template <int DP>
-__device__ __forceinline__ void tile_commit(char* slot, float* xn, int tid, const TileRegs<DP>& R) {
-  using TR = TileRegs<DP>;
-  using LY = Lay<DP>;
+__device__ __forceinline__ void tile_dma(const KArgs& a, const TileIdx<DP>& I, char* slot, float* xn,
+                                         int wave, int lane) {
+  using GA = Gather<DP>;
+  // Every address first: the compiler's wait for the index registers (loaded last iteration)
+  // must come before the first DMA, or it would also wait for the DMA (untracked, in order).
+  const uint16_t* src[GA::PER];
 #pragma unroll
-  for (int i = 0; i < TR::PER; ++i) {
-    const int e = tid + NT * i;
-    if (e < TR::NCH) {
-      const int row = e / TR::CPR, c = e - (e / TR::CPR) * TR::CPR;
-      const int part = c / (DP / 8), ch = c - part * (DP / 8);
-      *reinterpret_cast<u32x4*>(slot + part * LY::IMG + xoff<DP>(row, ch)) = R.v[i];
-    }
+  for (int j = 0; j < GA::PER; ++j) {
+    const int k = wave + NW * j;
+    const int B = 1024 * k + 16 * lane;
+    const int part = B / GA::IMG, off = B - part * GA::IMG;
+    const int row = off / GA::ROWB, ch = ((off % GA::ROWB) >> 4) ^ xsw<DP>(row);
+    src[j] = a.Xhl + static_cast<size_t>(I.src[j]) * (2 * DP) + part * DP + 8 * ch;
   }
-  if (tid < RT) xn[tid] = R.xn;
+  const float* xsrc = a.xnorm + I.xsrc;
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < GA::PER; ++j)
+    if (wave + NW * j < GA::NI) dma_piece(src[j], slot + 1024 * (wave + NW * j), 16);  // wave-uniform
+  if (wave == NW - 1) dma_piece(xsrc, xn, 4);
 }
+
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // A fragments of one centroid slot: lane (r, h) holds dims 16s + 8h + j of its slot's centre.
 template <int DP>
@@ -278,7 +324,7 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, int off, con
   float mymax = 0.f;
   for (int r = tid; r < m; r += NT) {
     const float* x = a.X + static_cast<size_t>(idx[r]) * DP;
-    const float* c = cen + (S.cenoff[p] + glab[static_cast<size_t>(p) * m + r]) * DP;
+    const float* c = cen + (S.cenoff[p] + glab[static_cast<size_t>(p) * a.lsm + r]) * DP;
     float s = 0.f;
     for (int d = 0; d < a.dreal; ++d) {
       const float t = x[d] - c[d];
@@ -333,7 +379,7 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, int off, con
         gv = S.red_v[w];
         gi = S.red_i[w];
       }
-    const int old = glab[static_cast<size_t>(p) * m + gi];
+    const int old = glab[static_cast<size_t>(p) * a.lsm + gi];
     const float* x = a.X + static_cast<size_t>(idx[gi]) * DP;
     for (int d = tid; d < DP; d += NT) {
       Sm[(off + old) * DP + d] -= x[d];
@@ -421,24 +467,32 @@ struct EState {
   unsigned chmask;
 };
 
-__device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, int t, int T, int nitems,
+// Loads the E-step operands of tile tp (issued one iteration before the E-step of tp): the
+// dword holding the old label (Lloyd; glab rows are 4-aligned, the byte is extracted at use)
+// or the closest distance (seeding).  One load instruction per item for both kinds, so no
+// two loads target one VGPR under divergent branches (that forces a vmcnt(0) wait).
+__device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, int tp, int T, int nitems,
                                                int tidl, const uint8_t* glab, const float* dbuf, int T1,
                                                unsigned (&pre)[NS]) {
   const int m = a.m;
-  const int erow = (t - 1) * RT + (tidl & (RT - 1));
-  const bool eok = (t >= 1 && t <= T) && erow < m;
+  const int erow = tp * RT + (tidl & (RT - 1));
+  const bool eok = (tp >= 0 && tp < T) && erow < m;
   const int eql = tidl >> 5;
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     pre[i] = 0;
     const int it = eql + 16 * i;
+#ifndef KM_EXP_NOPRE
     if (eok && it < nitems) {
       const int kind = S.ikind[it], p = S.iprob[it];
+      const unsigned* src = nullptr;
       if (kind == IK_RUN)
-        pre[i] = glab[static_cast<size_t>(p) * m + erow];
+        src = reinterpret_cast<const unsigned*>(glab + static_cast<size_t>(p) * a.lsm + (erow & ~3));
       else if (kind == IK_SEED)
-        pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(S.sslot[p]) * T1 + S.cs[p]) * m + erow]);
+        src = reinterpret_cast<const unsigned*>(dbuf + (static_cast<size_t>(S.sslot[p]) * T1 + S.cs[p]) * m + erow);
+      if (src) pre[i] = *src;
     }
+#endif
   }
 }
 
@@ -455,7 +509,7 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
   const bool eok = erow < m;
   const float* drow = Dt + (te & 1) * (RT * DSD) + ler * DSD;
   uint8_t* lsb = Ls + (te & 1) * (IMAX * RT);
-  const float xnr = XN[(te % NRING) * RT + ler];
+  const float xnr = XN[(te % NRING) * 64 + ler];
 #pragma unroll
   for (int i = 0; i < NS; ++i) {
     const int it = eql + 16 * i;
@@ -478,8 +532,10 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
           }
       }
       if (eok) {
-        if (kind == IK_RUN && pre[i] != static_cast<unsigned>(lab)) es.chmask |= 1u << i;
-        glab[static_cast<size_t>(p) * m + erow] = static_cast<uint8_t>(lab);
+        if (kind == IK_RUN && ((pre[i] >> (8 * (erow & 3))) & 0xFFu) != static_cast<unsigned>(lab)) es.chmask |= 1u << i;
+#ifndef KM_EXP_NOSTORE
+        glab[static_cast<size_t>(p) * a.lsm + erow] = static_cast<uint8_t>(lab);
+#endif
         es.iacc[i] += static_cast<double>(xnr) + static_cast<double>(best);
       }
       lsb[it * RT + ler] = eok ? static_cast<uint8_t>(lab) : 0xFF;
@@ -649,7 +705,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     }
     __syncthreads();
     const int P = S.P;
-    for (size_t e = tid; e < static_cast<size_t>(P) * m; e += NT) glab[e] = 0xFF;
+    for (size_t e = tid; e < static_cast<size_t>(P) * a.lsm; e += NT) glab[e] = 0xFF;
 
     // ---- tol = tol_rel * mean(var(X_sub, axis=0)) (sklearn _tolerance, :270-278) --
     {
@@ -690,6 +746,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
 
     // ---- sweeps -----------------------------------------------------------------
     for (;;) {
+      KM_STAMP(swp);
       if (tid == 0) schedule(a, S, idx);
       __syncthreads();
       const int nitems = S.nitems, ncols = S.ncols;
@@ -727,19 +784,35 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         mycl = S.scl[sl];
       }
       const bool mact = __ballot(mycl >= 0) != 0ull;  // wave-uniform: any running centre
+      // pipeline prologue: tile 0 in the ring, indices of tile 1
+      TileIdx<DP> nI;
       {
-        TileRegs<DP> R;
-        tile_issue<DP>(a, idx, 0, tid, R);
-        tile_commit<DP>(ring, XN, tid, R);
+        TileIdx<DP> I0;
+        idx_issue<DP>(a, idx, 0, wave, lane, I0);
+        tile_dma<DP>(a, I0, ring, XN, wave, lane);
+        idx_issue<DP>(a, idx, RT, wave, lane, nI);
+        dma_wait();
       }
+      unsigned pre[NS];  // E-step operands of tile t-1 (loaded in iteration t-1)
+#pragma unroll
+      for (int i = 0; i < NS; ++i) pre[i] = 0;
+#ifdef CC_KM_STAMPS
+      unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
       __syncthreads();
+      KM_STAMP(sw0);
+      KM_ACC(6, swp, sw0);
       for (int t = 0; t <= T + 1; ++t) {
+        KM_STAMP(s0);
         int tidl = tid;
         asm volatile("" : "+v"(tidl));
-        TileRegs<DP> R;
-        if (t + 1 < T) tile_issue<DP>(a, idx, (t + 1) * RT, tidl, R);
-        unsigned pre[NS];
-        estep_prefetch(a, S, t, T, nitems, tidl, glab, dbuf, T1, pre);
+        // gather: rows of tile t+1 by LDS-DMA (indices loaded last iteration), indices of
+        // tile t+2; E-step operands of tile t (consumed next iteration)
+        if (t + 1 < T) tile_dma<DP>(a, nI, ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * 64, wave, lane);
+        if (t + 2 < T) idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
+        unsigned npre[NS];
+        estep_prefetch(a, S, t, T, nitems, tidl, glab, dbuf, T1, npre);
+        KM_STAMP(s1);
         // distances of tile t (MFMA) -> D[t & 1]
         if (tact && t < T) {
           const char* xs = ring + (t % NRING) * LY::SLOT;
@@ -762,7 +835,9 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
             drow[i] = cn[i] - a.dscale * acc[v];
           }
         }
+        KM_STAMP(s2);
         estep<DP>(a, S, t, T, nitems, tidl, Dt, Ls, XN, glab, dbuf, tsum, T1, pre, es);
+        KM_STAMP(s3);
         // M-step of tile t-2 (one-hot x X on f16 MFMA; counts by popcount)
         if (mact && t >= 2) {
           const int tm = t - 2;
@@ -803,9 +878,24 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
             }
           }
         }
-        if (t + 1 < T) tile_commit<DP>(ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * RT, tidl, R);
+        KM_STAMP(s4);
+        dma_wait();  // tile t+1, the E-step operands and this iteration's stores have landed
+        KM_STAMP(s5);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) pre[i] = npre[i];
         __syncthreads();
+        KM_STAMP(s6);
+        KM_ACC(0, s0, s1);
+        KM_ACC(1, s1, s2);
+        KM_ACC(2, s2, s3);
+        KM_ACC(3, s3, s4);
+        KM_ACC(4, s4, s5);
+        KM_ACC(5, s5, s6);
       }
+#ifdef CC_KM_STAMPS
+      if (blockIdx.x == 0 && lane == 0 && a.stats)
+        for (int k = 0; k < 7; ++k) atomicAdd(&a.stats[8 + 8 * wave + k], st_acc[k]);
+#endif
       estep_finish(S, nitems, tid, es);
       // sums -> Sm (aliases the ring and D: every reader passed the last barrier); counts
       if (mact) {
@@ -821,6 +911,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       }
       __syncthreads();
 
+      KM_STAMP(pp0);
       // ---- seeding decisions (thread per problem) -----------------------------------
       if (tid < P) {
         const int p = tid;
@@ -1001,6 +1092,10 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         }
       }
       __syncthreads();
+#ifdef CC_KM_STAMPS
+      KM_STAMP(pp1);
+      if (blockIdx.x == 0 && tid == 0 && a.stats) atomicAdd(&a.stats[73], pp1 - pp0);
+#endif
     }
 
     // ---- best of n_init per K, output (KMeans.fit :1495-1531) -------------------
@@ -1013,8 +1108,8 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         if (tid <= KMAX) S.map[tid] = -1;
         if (tid == 0) S.flag = 0;
         __syncthreads();
-        const uint8_t* l1 = glab + static_cast<size_t>(p) * m;
-        const uint8_t* l2 = glab + static_cast<size_t>(best) * m;
+        const uint8_t* l1 = glab + static_cast<size_t>(p) * a.lsm;
+        const uint8_t* l2 = glab + static_cast<size_t>(best) * a.lsm;
         for (int r = tid; r < m; r += NT) S.map[l1[r]] = l2[r];
         __syncthreads();
         bool bad = false;
@@ -1025,7 +1120,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         __syncthreads();
       }
       const int kidx = S.kidx[p0];
-      const uint8_t* lb = glab + static_cast<size_t>(best) * m;
+      const uint8_t* lb = glab + static_cast<size_t>(best) * a.lsm;
       uint8_t* out = a.labels_out + static_cast<size_t>(kidx) * a.n * a.ldl + h;
       for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = lb[r];
       if (tid == 0) {
@@ -1081,7 +1176,7 @@ WsLayout ws_layout(int m, int dpad, const int32_t* units, int nU, int seedmax) {
   }
   const int T = (m + RT - 1) / RT;
   auto al = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
-  L.off_cen = al(static_cast<size_t>(L.Pws) * m);
+  L.off_cen = al(static_cast<size_t>(L.Pws) * ((m + 63) & ~63));
   L.off_cenn = L.off_cen + al(static_cast<size_t>(L.Cws) * dpad * sizeof(float));
   L.off_cpos = L.off_cenn + al(static_cast<size_t>(L.Cws) * sizeof(float));
   L.off_dbuf = L.off_cpos + al(static_cast<size_t>(L.Pws) * L.Kws * sizeof(int32_t));
@@ -1279,6 +1374,7 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
   a.Kws = L.Kws;
   a.Tws = L.Tws;
   a.seedmax = seedmax;
+  a.lsm = (m + 63) & ~63;
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nU));
   switch (dpad) {
     case 32: launch<32>(a, blocks, st); break;

@@ -133,7 +133,7 @@ class BatchedKMeans:
         if Xhl is None:
             raise _lib.CCMIError("BatchedKMeans.run needs the f16 operand image (prepare_rows)")
         nh = h_end - h_begin
-        self.stats = torch.zeros(8, dtype=torch.int64, device=dev)
+        self.stats = torch.zeros(128, dtype=torch.int64, device=dev)  # [0:8] counters, rest: diagnostics
         if nh <= 0:
             return labels_nh
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
