@@ -44,6 +44,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <string>
@@ -63,12 +64,13 @@ constexpr int NT = 512;
 constexpr int NW = 8;
 constexpr int RT = 32;              // rows per tile (one MFMA row block)
 constexpr int CW = 256;             // centroid slots per sweep (8 waves x 32)
-constexpr int NS = 4;               // E-step work items per thread (16 item lanes x 8)
-constexpr int IMAX = 16 * NS;       // work items per sweep
+constexpr int NLS = 4;              // E-step Lloyd steps per wave (one Lloyd item each)
+constexpr int NSS = 4;              // E-step seeding steps per wave (two seeding items each)
+constexpr int IMAX = 64;            // work items per sweep
 constexpr int PMAX = CC_KM_PMAX;    // problems per unit
 constexpr int TMAX = 6;             // max local trials: 2 + floor(ln 127)
 constexpr int KMAX = 127;
-constexpr int DSD = CW + 1;         // distance-tile row stride (floats): conflict-free b32 reads
+constexpr int DSD = CW + 4;         // distance-tile row stride (floats): 16-B rows, conflict-free b128
 constexpr int NRING = 4;            // X tile ring: t+1 (gather), t (dist), t-2 (M-step)
 constexpr int US = CC_KM_USTRIDE;
 
@@ -111,7 +113,7 @@ struct KArgs {
   unsigned long long* stats;
   unsigned* counter;
   uint8_t* ws;
-  size_t ws_per_wg, off_cen, off_cenn, off_cpos, off_dbuf, off_tsum, off_rdist;
+  size_t ws_per_wg, off_cen, off_cenn, off_cpos, off_dbuf, off_rdist;
   int Pws, Kws, Tws, seedmax;
   int lsm;  // glab row stride (m rounded up to 64)
 };
@@ -124,7 +126,7 @@ struct State {
   unsigned seedfree;
   // problems
   unsigned char K[PMAX], kidx[PMAX], init[PMAX], ntr[PMAX], st[PMAX], c[PMAX], cs[PMAX], sslot[PMAX];
-  unsigned char need_sel[PMAX], to_run[PMAX], sbest[PMAX];
+  unsigned char need_sel[PMAX], to_run[PMAX], sbest[PMAX], lcur[PMAX];
   short cenoff[PMAX], pitem[PMAX];
   int iter[PMAX], amax[PMAX], nempty[PMAX];
   float pot32[PMAX], inert[PMAX];
@@ -132,12 +134,16 @@ struct State {
   // sweep
   int nitems, ncols;
   unsigned char ikind[IMAX], iprob[IMAX], itr[IMAX];
+  unsigned iw0[IMAX], iw1[IMAX];               // packed item words (see EState)
+  unsigned char lstep[NW][NLS], sstep[NW][NSS][2];  // E-step steps of each wave (item; 0xFF none)
+  unsigned char nlw[NW], nsw[NW];
   short ioff[IMAX], incol[IMAX];
   double iinert[IMAX];
   unsigned ichanged[IMAX];
   short sitem[CW], scl[CW];
   int srow[CW];  // >= 0: X row (seeding candidate); < 0: -(centre row) - 1
-  float cnorm[CW], shift[CW];
+  alignas(16) float cnorm[CW];
+  float shift[CW];
   unsigned cnt[CW];
   // scratch
   double red_v[NW];
@@ -156,7 +162,7 @@ struct Lay {
   static constexpr int U_END = OFF_D + 2 * DBUF;
   static constexpr int S_BYTES = CW * DP * 4;  // centre sums [CW][DP] f32, aliasing ring + D
   static_assert(S_BYTES <= U_END, "centre sums must fit in the ring + distance tiles");
-  static constexpr int OFF_LS = (U_END + 15) / 16 * 16;  // labels [2][IMAX][RT] u8
+  static constexpr int OFF_LS = (U_END + 32 + 15) / 16 * 16;  // labels [2][IMAX][RT] u8 (32 B slack: E-step over-reads)
   static constexpr int OFF_XN = OFF_LS + 2 * IMAX * RT;  // row norms [NRING][64] f32 (DMA'd, 32 used)
   static constexpr int OFF_ST = OFF_XN + NRING * 64 * 4;
   static constexpr int TOTAL = OFF_ST + ((sizeof(State) + 15) / 16) * 16;
@@ -257,14 +263,16 @@ __device__ __forceinline__ void idx_issue(const KArgs& a, const int32_t* idx, in
 // (the ds_read_b64_tr_b16 of the M-step), exposing the gather latency mid-iteration.
 // Untracked VMEM ops only make the compiler's own vmcnt waits stricter (the counter drains in
 // order); completion is awaited explicitly by dma_wait() before the barrier that publishes the
-// tile.  M0 is set inside the asm; no compiler-generated code in this kernel uses M0.
+// tile.  M0 is set inside the asm; no compiler-generated code in this kernel uses M0.  No
+// "memory" clobber: the piece writes a ring slot nothing touches until the next barrier and
+// reads immutable rows (a clobber makes the compiler drain vmcnt in front of every piece).
 __device__ __forceinline__ void dma_piece(const void* g, const void* lds_dst, int bytes) {
   const unsigned la = static_cast<unsigned>(reinterpret_cast<uintptr_t>(
       (__attribute__((address_space(3))) const char*)lds_dst));
   if (bytes == 16)
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g) : "memory");
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g));
   else
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g) : "memory");
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g));
 }
 
 template <int DP>
@@ -274,10 +282,12 @@ __device__ __forceinline__ void tile_dma(const KArgs& a, const TileIdx<DP>& I, c
   // Every address first: the compiler's wait for the index registers (loaded last iteration)
   // must come before the first DMA, or it would also wait for the DMA (untracked, in order).
   const uint16_t* src[GA::PER];
+  int ln = lane;
+  asm volatile("" : "+v"(ln));  // recompute the per-lane chunk offsets (cheap) rather than hold them
 #pragma unroll
   for (int j = 0; j < GA::PER; ++j) {
     const int k = wave + NW * j;
-    const int B = 1024 * k + 16 * lane;
+    const int B = 1024 * k + 16 * ln;
     const int part = B / GA::IMG, off = B - part * GA::IMG;
     const int row = off / GA::ROWB, ch = ((off % GA::ROWB) >> 4) ^ xsw<DP>(row);
     src[j] = a.Xhl + static_cast<size_t>(I.src[j]) * (2 * DP) + part * DP + 8 * ch;
@@ -291,6 +301,19 @@ __device__ __forceinline__ void tile_dma(const KArgs& a, const TileIdx<DP>& I, c
 }
 
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Wait for this iteration's DMA pieces and loads but not for the label/potential stores the
+// E-step issued after them (vmcnt drains in order; `younger` = store instructions issued
+// after the last load, wave-uniform): store acks would otherwise be exposed every tile.
+__device__ __forceinline__ void dma_wait_leaving(int younger) {
+  if (younger >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (younger >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (younger >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (younger >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (younger >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (younger >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // A fragments of one centroid slot: lane (r, h) holds dims 16s + 8h + j of its slot's centre.
 template <int DP>
@@ -316,7 +339,7 @@ __device__ __forceinline__ void afrag_load(h8 (&ah)[DP / 16], h8 (&al)[DP / 16],
 
 // Empty-cluster relocation for problem p (rare path; _k_means_common.pyx:167-212).
 // Sm holds the un-averaged sums of the problem's slots [off, off+K), cen the centres the
-// labels came from.
+// labels came from, glab the problem's labels of this sweep.
 template <int DP>
 __device__ void relocate(const KArgs& a, const int32_t* idx, int p, int off, const float* cen,
                          float* Sm, State& S, const uint8_t* glab, float* dist, int tid) {
@@ -324,7 +347,7 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, int off, con
   float mymax = 0.f;
   for (int r = tid; r < m; r += NT) {
     const float* x = a.X + static_cast<size_t>(idx[r]) * DP;
-    const float* c = cen + (S.cenoff[p] + glab[static_cast<size_t>(p) * a.lsm + r]) * DP;
+    const float* c = cen + (S.cenoff[p] + glab[r]) * DP;
     float s = 0.f;
     for (int d = 0; d < a.dreal; ++d) {
       const float t = x[d] - c[d];
@@ -379,7 +402,7 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, int off, con
         gv = S.red_v[w];
         gi = S.red_i[w];
       }
-    const int old = glab[static_cast<size_t>(p) * a.lsm + gi];
+    const int old = glab[gi];
     const float* x = a.X + static_cast<size_t>(idx[gi]) * DP;
     for (int d = tid; d < DP; d += NT) {
       Sm[(off + old) * DP + d] -= x[d];
@@ -398,10 +421,10 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, int off, con
 
 // k-means++ candidate positions for centre S.c[p] (>= 1) of problem p, one wave:
 // searchsorted(cumsum(closest), u * pot) (side='left': #{cumsum < v}), clipped to m-1.
-// The cumsum is blocked: f64 prefix over the per-tile sums of the chosen candidate
-// (written by the E-step), then an f64 running sum inside the crossing tile.
-__device__ void kpp_select(const KArgs& a, State& S, int p, const float* closest,
-                           const double* tsum, int lane) {
+// The cumsum is blocked by 32-row tiles: each lane sums whole tiles sequentially in f64 (the
+// in-tile order of the sklearn cumsum), the wave prefix-sums the tile sums, and the crossing
+// tile is walked sequentially from its prefix, so the two levels agree exactly.
+__device__ void kpp_select(const KArgs& a, State& S, int p, const float* closest, int lane) {
   const int ntr = S.ntr[p], c = S.c[p], m = a.m, T = a.T;
   const double* u = a.kpp_u + (static_cast<size_t>(S.kidx[p]) * a.n_init + S.init[p]) * a.kpp_stride +
                     1 + static_cast<size_t>(c - 1) * ntr;
@@ -419,7 +442,18 @@ __device__ void kpp_select(const KArgs& a, State& S, int p, const float* closest
   double run = 0.0;
   for (int b = 0; b < T; b += 64) {
     const int j = b + lane;
-    double v = (j < T) ? tsum[j] : 0.0;
+    double v = 0.0;
+    if (j < T) {
+      const float* rowp = closest + RT * j;
+      const int nr = min(RT, m - RT * j);
+      for (int r = 0; r < nr; r += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(rowp + r);  // m, RT multiples of 4 or tail
+        v += static_cast<double>(q.x);
+        if (r + 1 < nr) v += static_cast<double>(q.y);
+        if (r + 2 < nr) v += static_cast<double>(q.z);
+        if (r + 3 < nr) v += static_cast<double>(q.w);
+      }
+    }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const double y = __shfl_up(v, o);
@@ -440,7 +474,7 @@ __device__ void kpp_select(const KArgs& a, State& S, int p, const float* closest
     }
     run = __shfl(cum, 63);
   }
-  // within the crossing tile: lane t walks its 32 rows
+  // within the crossing tile: lane t walks its rows
 #pragma unroll
   for (int t = 0; t < TMAX; ++t) {
     if (t >= ntr || lane != t) continue;
@@ -459,117 +493,142 @@ __device__ void kpp_select(const KArgs& a, State& S, int p, const float* closest
   }
 }
 
-// ---- E-step (all 512 threads): thread = (row er = tid & 31, item lane eq = tid >> 5), items
-// eq + 16 i.  Lloyd items: argmin over the problem's K slots (strict <, lowest index), label
-// change, inertia; seeding items: min with the closest distance, potential, tile sums.
+// ---- E-step (all 512 threads): lane = (tile row tid & 31, half-wave hh).  The schedule deals
+// the sweep's work items to the 8 waves (LPT by cost) as STEPS:
+//   Lloyd steps (one item, wave-uniform): the two half-waves scan the two halves of the item's
+//     slots in aligned 4-slot chunks (problems sit at 4-aligned slot offsets, K padded to a
+//     multiple of 4 with +inf dummy slots, so no masking) and merge with v_permlane32_swap;
+//     half-wave 0 stores the label (global, double-buffered per problem: the "labels
+//     changed" test is a post-sweep compare of the two buffers) and the M-step label (LDS)
+//     and accumulates the inertia;
+//   seeding steps (two items, one per half-wave): min with the closest distance, stored for
+//     the potential and the next k-means++ draw.
+// Item words (LDS):
+//   iw0 = label buffer<<30 | kind<<24 | problem<<16 | K<<8 | slot offset
+//   iw1 = dbuf write slot<<11 | closest slot<<8 | trial<<5 | seeding slot
 struct EState {
-  double iacc[NS];
-  unsigned chmask;
+  double iaccL[NLS], iaccS[NSS];
 };
 
-// Loads the E-step operands of tile tp (issued one iteration before the E-step of tp): the
-// dword holding the old label (Lloyd; glab rows are 4-aligned, the byte is extracted at use)
-// or the closest distance (seeding).  One load instruction per item for both kinds, so no
-// two loads target one VGPR under divergent branches (that forces a vmcnt(0) wait).
-__device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, int tp, int T, int nitems,
-                                               int tidl, const uint8_t* glab, const float* dbuf, int T1,
-                                               unsigned (&pre)[NS]) {
+__device__ __forceinline__ int iw_off(unsigned w) { return w & 0xFF; }
+__device__ __forceinline__ int iw_K(unsigned w) { return (w >> 8) & 0xFF; }
+__device__ __forceinline__ int iw_prob(unsigned w) { return (w >> 16) & 0x3F; }
+__device__ __forceinline__ int iw_kind(unsigned w) { return (w >> 24) & 3; }
+__device__ __forceinline__ int iw_buf(unsigned w) { return (w >> 30) & 1; }
+
+// Closest distances of the seeding items of tile tp (issued one iteration before its E-step).
+__device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, int tp, int T, int tidl,
+                                               const float* dbuf, int T1, unsigned (&pre)[NSS]) {
   const int m = a.m;
   const int erow = tp * RT + (tidl & (RT - 1));
   const bool eok = (tp >= 0 && tp < T) && erow < m;
-  const int eql = tidl >> 5;
+  const int w = (tidl >> 6) & 7, hh = (tidl >> 5) & 1;  // tidl is opaque: steps re-read from LDS
+  const int ns = __builtin_amdgcn_readfirstlane(S.nsw[w]);
 #pragma unroll
-  for (int i = 0; i < NS; ++i) {
+  for (int i = 0; i < NSS; ++i) {
     pre[i] = 0;
-    const int it = eql + 16 * i;
-#ifndef KM_EXP_NOPRE
-    if (eok && it < nitems) {
-      const int kind = S.ikind[it], p = S.iprob[it];
-      const unsigned* src = nullptr;
-      if (kind == IK_RUN)
-        src = reinterpret_cast<const unsigned*>(glab + static_cast<size_t>(p) * a.lsm + (erow & ~3));
-      else if (kind == IK_SEED)
-        src = reinterpret_cast<const unsigned*>(dbuf + (static_cast<size_t>(S.sslot[p]) * T1 + S.cs[p]) * m + erow);
-      if (src) pre[i] = *src;
+    if (i >= ns) break;
+    const int it = S.sstep[w][i][hh];
+    if (eok && it != 0xFF && iw_kind(S.iw0[it]) == IK_SEED) {
+      const unsigned w1 = S.iw1[it];
+      pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 8) & 7)) * a.lsm + erow]);
     }
-#endif
   }
 }
 
+// strict-< argmin update of (best, lab) with the 4 values of an aligned chunk at slot c
+__device__ __forceinline__ void amin4(const float4& v, int c, float& best, int& lab) {
+  if (v.x < best) { best = v.x; lab = c; }
+  if (v.y < best) { best = v.y; lab = c + 1; }
+  if (v.z < best) { best = v.z; lab = c + 2; }
+  if (v.w < best) { best = v.w; lab = c + 3; }
+}
+
 template <int DP>
-__device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int T, int nitems, int tidl,
-                                      const float* Dt, uint8_t* Ls, const float* XN, uint8_t* glab,
-                                      float* dbuf, double* tsum, int T1, const unsigned (&pre)[NS],
+__device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int T, int tidl, const float* Dt,
+                                      uint8_t* Ls, const float* XN, uint8_t* glab, float* dbuf, int T1,
+                                      const unsigned (&pre)[NSS], const unsigned (&lw)[NLS], int nl,
                                       EState& es) {
   if (t < 1 || t > T) return;
   const int m = a.m;
   const int te = t - 1;
-  const int ler = tidl & (RT - 1), eql = tidl >> 5;
+  const int ler = tidl & (RT - 1);
+  const int w = (tidl >> 6) & 7, hh = (tidl >> 5) & 1;
   const int erow = te * RT + ler;
   const bool eok = erow < m;
   const float* drow = Dt + (te & 1) * (RT * DSD) + ler * DSD;
   uint8_t* lsb = Ls + (te & 1) * (IMAX * RT);
   const float xnr = XN[(te % NRING) * 64 + ler];
+  constexpr float INF = __builtin_huge_valf();
+  // Lloyd steps (wave-uniform words, hoisted for the sweep)
 #pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    const int it = eql + 16 * i;
-    if (it >= nitems) continue;  // uniform per half-wave
-    const int kind = S.ikind[it], p = S.iprob[it], off = S.ioff[it];
-    if (kind >= IK_RUN) {
-      const int K = S.incol[it];
-      const float* dr = drow + off;
-      float best = dr[0];
-      int lab = 0;
-      for (int c0 = 1; c0 < K; c0 += 8) {  // 8 loads in flight, then strict-< scan
-        float v[8];
+  for (int i = 0; i < NLS; ++i) {
+    if (i >= nl) break;
+    const unsigned ww = lw[i];
+    const int it = S.lstep[w][i];
+    const int off = iw_off(ww), C = (iw_K(ww) + 3) >> 2, h0 = (C + 1) >> 1;
+    const int base = off + (hh ? 4 * h0 : 0), cnt = hh ? C - h0 : h0;
+    float best = INF;
+    int lab = 0;
+    for (int j0 = 0; j0 < h0; j0 += 4) {  // 4 chunk reads in flight, then the compare chain
+      int col[4];
+      float4 v[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = dr[min(c0 + j, K - 1)];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (c0 + j < K && v[j] < best) {
-            best = v[j];
-            lab = c0 + j;
-          }
+      for (int u = 0; u < 4; ++u) {
+        col[u] = (j0 + u < cnt) ? base + 4 * (j0 + u) : CW;  // CW..CW+3 hold +inf
+        v[u] = *reinterpret_cast<const float4*>(drow + col[u]);
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) amin4(v[u], col[u], best, lab);
+    }
+    // merge the halves (v_permlane32_swap: lane i <-> i^32 without LDS): lower value, ties to
+    // the lower slot (half 0 holds the lower slots)
+    const auto bs = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+    const auto ls = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(lab), static_cast<unsigned>(lab), false, false);
+    const float ob = __uint_as_float(hh ? bs[0] : bs[1]);
+    const int ol = static_cast<int>(hh ? ls[0] : ls[1]);
+    if (ob < best || (ob == best && ol < lab)) {
+      best = ob;
+      lab = ol;
+    }
+    lab -= off;
+    if (hh == 0) {
       if (eok) {
-        if (kind == IK_RUN && ((pre[i] >> (8 * (erow & 3))) & 0xFFu) != static_cast<unsigned>(lab)) es.chmask |= 1u << i;
-#ifndef KM_EXP_NOSTORE
-        glab[static_cast<size_t>(p) * a.lsm + erow] = static_cast<uint8_t>(lab);
-#endif
-        es.iacc[i] += static_cast<double>(xnr) + static_cast<double>(best);
+        glab[(static_cast<size_t>(2 * iw_prob(ww) + iw_buf(ww))) * a.lsm + erow] = static_cast<uint8_t>(lab);
+        es.iaccL[i] += static_cast<double>(xnr) + static_cast<double>(best);
       }
       lsb[it * RT + ler] = eok ? static_cast<uint8_t>(lab) : 0xFF;
-    } else {
-      const int tr = S.itr[it], ss = S.sslot[p];
-      const float dist = fmaxf(xnr + drow[off], 0.f);
-      float dm = dist;
-      int slot = 0;
-      if (kind == IK_SEED) {
-        dm = fminf(__uint_as_float(pre[i]), dist);
-        const int cs = S.cs[p];
-        slot = (tr < cs) ? tr : tr + 1;
-      }
-      const double dv = eok ? static_cast<double>(dm) : 0.0;
-      if (eok) dbuf[(static_cast<size_t>(ss) * T1 + slot) * m + erow] = dm;
-      es.iacc[i] += dv;
-      const double ts = half_sum(dv);
-      if (ler == 0) tsum[(static_cast<size_t>(ss) * a.Tws + tr) * T + te] = ts;
+    }
+  }
+  // seeding steps (one item per half-wave)
+  const int ns = __builtin_amdgcn_readfirstlane(S.nsw[w]);
+#pragma unroll
+  for (int i = 0; i < NSS; ++i) {
+    if (i >= ns) break;
+    const int it = S.sstep[w][i][hh];
+    const bool has = it != 0xFF;
+    const unsigned ww = has ? S.iw0[it] : 0u, w1 = has ? S.iw1[it] : 0u;
+    const float dist = fmaxf(xnr + drow[iw_off(ww)], 0.f);
+    const float dm = (iw_kind(ww) == IK_SEED) ? fminf(__uint_as_float(pre[i]), dist) : dist;
+    if (eok && has) {
+      dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 11) & 7)) * a.lsm + erow] = dm;
+      es.iaccS[i] += static_cast<double>(dm);
     }
   }
 }
 
-__device__ __forceinline__ void estep_finish(State& S, int nitems, int tid, const EState& es) {
-  const int er = tid & (RT - 1), eq = tid >> 5, hh = (tid & 63) >> 5;
+__device__ __forceinline__ void estep_finish(State& S, int tid, const EState& es) {
+  const int er = tid & (RT - 1), hh = (tid >> 5) & 1, w = tid >> 6;
+  const int nl = S.nlw[w], ns = S.nsw[w];
 #pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    const int it = eq + 16 * i;
-    const double v = half_sum(es.iacc[i]);
-    const unsigned long long bal = __ballot((es.chmask >> i) & 1u);
-    const unsigned halfbits = static_cast<unsigned>(bal >> (32 * hh));
-    if (it < nitems && er == 0) {
-      S.iinert[it] = v;
-      S.ichanged[it] = halfbits != 0u;
-    }
+  for (int i = 0; i < NLS; ++i) {
+    const double v = half_sum(es.iaccL[i]);
+    if (i < nl && er == 0 && hh == 0) S.iinert[S.lstep[w][i]] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < NSS; ++i) {
+    const double v = half_sum(es.iaccS[i]);
+    if (i < ns && er == 0 && S.sstep[w][i][hh] != 0xFF) S.iinert[S.sstep[w][i][hh]] = v;
   }
 }
 
@@ -586,21 +645,29 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     S.st[p] = ST_SEED;
     S.c[p] = 0;
   }
-  int ni = 0, nc = 0;
+  int ni = 0, nc = 0, nls = 0, nss2 = 0;  // items, slots, Lloyd steps, seeding half-steps
   unsigned long long nseed = 0, nlloyd = 0, nm = 0;
   for (int p = 0; p < P; ++p) S.pitem[p] = -1;
   for (int p = 0; p < P; ++p) {
     if (S.st[p] != ST_SEED) continue;
     const int c = S.c[p];
     const int nt = (c == 0) ? 1 : S.ntr[p];
-    if (nc + nt > CW || ni + nt > IMAX) continue;
+    if (nc + nt > CW || ni + nt > IMAX || nss2 + nt > 2 * NW * NSS) continue;
+    nss2 += nt;
     S.pitem[p] = static_cast<short>(ni);
     for (int t = 0; t < nt; ++t) {
-      S.ikind[ni] = static_cast<unsigned char>(c == 0 ? IK_SEED0 : IK_SEED);
+      const int kind = (c == 0) ? IK_SEED0 : IK_SEED;
+      S.ikind[ni] = static_cast<unsigned char>(kind);
       S.iprob[ni] = static_cast<unsigned char>(p);
       S.ioff[ni] = static_cast<short>(nc);
       S.incol[ni] = 1;
       S.itr[ni] = static_cast<unsigned char>(t);
+      const int cs = (kind == IK_SEED0) ? 0 : S.cs[p];
+      const int wslot = (kind == IK_SEED0) ? 0 : ((t < cs) ? t : t + 1);
+      S.iw0[ni] = (static_cast<unsigned>(kind) << 24) | (static_cast<unsigned>(p) << 16) | (1u << 8) |
+                  static_cast<unsigned>(nc);
+      S.iw1[ni] = (static_cast<unsigned>(wslot) << 11) | (static_cast<unsigned>(cs) << 8) |
+                  (static_cast<unsigned>(t) << 5) | static_cast<unsigned>(S.sslot[p]);
       const int pos = (c == 0) ? a.kpp_pos[S.kidx[p] * a.n_init + S.init[p]] : S.cand[p][t];
       S.sitem[nc] = static_cast<short>(ni);
       S.scl[nc] = -1;
@@ -610,34 +677,77 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     }
     nseed += static_cast<unsigned long long>(nt) * a.m;
   }
+  // Lloyd problems: 4-aligned offsets, K padded to a multiple of 4 with dummy (+inf) slots
   int first_skip = -1, last = -1;
   for (int j = 0; j < P; ++j) {
     const int p = (S.rr + j) % P;
     const int st = S.st[p];
     if (st != ST_RUN && st != ST_FINAL) continue;
-    const int K = S.K[p];
-    if (nc + K > CW || ni + 1 > IMAX) {
+    const int K = S.K[p], K4 = (K + 3) & ~3;
+    const int off = (nc + 3) & ~3;
+    if (off + K4 > CW || ni + 1 > IMAX || nls + 1 > NW * NLS) {
       if (first_skip < 0) first_skip = p;
       continue;
     }
+    for (int c = nc; c < off; ++c) {  // alignment gap
+      S.sitem[c] = -1;
+      S.scl[c] = -1;
+      S.srow[c] = INT_MIN;
+    }
     S.pitem[p] = static_cast<short>(ni);
-    S.ikind[ni] = static_cast<unsigned char>(st == ST_RUN ? IK_RUN : IK_FINAL);
+    const int kind = (st == ST_RUN) ? IK_RUN : IK_FINAL;
+    S.ikind[ni] = static_cast<unsigned char>(kind);
     S.iprob[ni] = static_cast<unsigned char>(p);
-    S.ioff[ni] = static_cast<short>(nc);
+    S.ioff[ni] = static_cast<short>(off);
     S.incol[ni] = static_cast<short>(K);
     S.itr[ni] = 0;
-    for (int c = 0; c < K; ++c) {
-      S.sitem[nc + c] = static_cast<short>(ni);
-      S.scl[nc + c] = static_cast<short>(st == ST_RUN ? c : -1);
-      S.srow[nc + c] = -(S.cenoff[p] + c) - 1;
+    S.iw0[ni] = (static_cast<unsigned>(1 - S.lcur[p]) << 30) | (static_cast<unsigned>(kind) << 24) |
+                (static_cast<unsigned>(p) << 16) | (static_cast<unsigned>(K) << 8) | static_cast<unsigned>(off);
+    S.iw1[ni] = 0;
+    for (int c = 0; c < K4; ++c) {
+      S.sitem[off + c] = static_cast<short>(c < K ? ni : -1);
+      S.scl[off + c] = static_cast<short>((st == ST_RUN && c < K) ? c : -1);
+      S.srow[off + c] = (c < K) ? -(S.cenoff[p] + c) - 1 : INT_MIN;
     }
     ++ni;
-    nc += K;
+    ++nls;
+    nc = off + K4;
     last = p;
     nlloyd += static_cast<unsigned long long>(K) * a.m;
     if (st == ST_RUN) nm += a.m;
   }
   S.rr = (first_skip >= 0) ? first_skip : (last >= 0 ? (last + 1) % P : S.rr);
+  // deal the steps to the waves (LPT: heaviest first onto the least loaded wave)
+  int wcost[NW];
+  for (int w = 0; w < NW; ++w) {
+    wcost[w] = 0;
+    S.nlw[w] = S.nsw[w] = 0;
+    for (int i = 0; i < NLS; ++i) S.lstep[w][i] = 0xFF;
+    for (int i = 0; i < NSS; ++i) S.sstep[w][i][0] = S.sstep[w][i][1] = 0xFF;
+  }
+  for (int it = 0; it < ni; ++it) {  // Lloyd items were appended after the seeding items
+    if (S.ikind[it] < IK_RUN) continue;
+    int w = -1;
+    for (int q = 0; q < NW; ++q)
+      if (S.nlw[q] < NLS && (w < 0 || wcost[q] < wcost[w])) w = q;
+    S.lstep[w][S.nlw[w]++] = static_cast<unsigned char>(it);
+    wcost[w] += (S.incol[it] + 7) / 8 * 16 + 24;
+  }
+  int open_w = -1;
+  for (int it = 0; it < ni; ++it) {
+    if (S.ikind[it] >= IK_RUN) continue;
+    if (open_w >= 0) {  // second half of an open seeding step
+      S.sstep[open_w][S.nsw[open_w] - 1][1] = static_cast<unsigned char>(it);
+      open_w = -1;
+      continue;
+    }
+    int w = -1;
+    for (int q = 0; q < NW; ++q)
+      if (S.nsw[q] < NSS && (w < 0 || wcost[q] < wcost[w])) w = q;
+    S.sstep[w][S.nsw[w]++][0] = static_cast<unsigned char>(it);
+    wcost[w] += 20;
+    open_w = w;
+  }
   S.nitems = ni;
   S.ncols = nc;
   S.n_seed += nseed;
@@ -669,7 +779,6 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
   float* cenn = reinterpret_cast<float*>(wsb + a.off_cenn);             // [Cws]
   int32_t* cpos = reinterpret_cast<int32_t*>(wsb + a.off_cpos);         // [Pws][Kws]
   float* dbuf = reinterpret_cast<float*>(wsb + a.off_dbuf);             // [seedmax][Tws+1][m]
-  double* tsum = reinterpret_cast<double*>(wsb + a.off_tsum);           // [seedmax][Tws][T]
   float* rdist = reinterpret_cast<float*>(wsb + a.off_rdist);           // [m]
   const int T1 = a.Tws + 1;
   if (tid == 0) S.n_lloyd = S.n_seed = S.n_mrows = S.n_reloc = S.n_sweeps = S.n_ctiles = 0;
@@ -697,6 +806,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         S.ntr[p] = static_cast<unsigned char>(gd[4 + 4 * p]);
         S.st[p] = ST_WAIT;
         S.iter[p] = 0;
+        S.lcur[p] = 0;
         S.cenoff[p] = static_cast<short>(o);
         o += S.K[p];
       }
@@ -705,7 +815,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     }
     __syncthreads();
     const int P = S.P;
-    for (size_t e = tid; e < static_cast<size_t>(P) * a.lsm; e += NT) glab[e] = 0xFF;
+    for (size_t e = tid; e < static_cast<size_t>(2 * P) * a.lsm; e += NT) glab[e] = 0xFF;  // 2 buffers per problem
 
     // ---- tol = tol_rel * mean(var(X_sub, axis=0)) (sklearn _tolerance, :270-278) --
     {
@@ -755,24 +865,34 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       // slot norms: centres from the last write-back, candidates from xnorm
       if (tid < ncols) {
         const int sr = S.srow[tid];
-        S.cnorm[tid] = (sr >= 0) ? a.xnorm[sr] : cenn[-sr - 1];
+        S.cnorm[tid] = (sr >= 0) ? a.xnorm[sr] : (sr == INT_MIN ? __builtin_huge_valf() : cenn[-sr - 1]);
       }
+      if (tid < 2 * RT * 4) Dt[(tid >> 2) * DSD + CW + (tid & 3)] = __builtin_huge_valf();  // +inf chunk
       // Every wave owns the slot tile ct = wave (32 slots): its centres as register-resident
       // f16 A fragments (distances) and its M-step sums as MFMA accumulators.
       const int ct = wave;
       const int hh = lane >> 5, lr = lane & 31;
       const int sl = 32 * ct + lr;
       EState es;
-      es.chmask = 0;
 #pragma unroll
-      for (int i = 0; i < NS; ++i) es.iacc[i] = 0.0;
+      for (int i = 0; i < NLS; ++i) es.iaccL[i] = 0.0;
+      // this wave's Lloyd step words, wave-uniform for the whole sweep
+      const int nl = __builtin_amdgcn_readfirstlane(S.nlw[wave]);
+      unsigned lw[NLS];
+#pragma unroll
+      for (int i = 0; i < NLS; ++i)
+        lw[i] = __builtin_amdgcn_readfirstlane(i < nl ? S.iw0[S.lstep[wave][i]] : 0u);
+#pragma unroll
+      for (int i = 0; i < NSS; ++i) es.iaccS[i] = 0.0;
       h8 ah[DP / 16], al[DP / 16];
       const bool tact = 32 * ct < ncols;  // wave-uniform
       {
-        int sr = 0;
+        int sr = INT_MIN;
         if (sl < ncols) sr = S.srow[sl];
-        const float* src = (sr >= 0) ? a.X + static_cast<size_t>(sr) * DP : cen + static_cast<size_t>(-sr - 1) * DP;
-        afrag_load<DP>(ah, al, src, sl < ncols, hh, a.scale);
+        const bool ok = sr != INT_MIN;  // dummy / alignment slots: zero centre, +inf norm
+        const float* src = (sr >= 0) ? a.X + static_cast<size_t>(sr) * DP
+                                     : cen + static_cast<size_t>(ok ? -sr - 1 : 0) * DP;
+        afrag_load<DP>(ah, al, src, ok, hh, a.scale);
       }
       v16f sacc[DP / 32];
 #pragma unroll
@@ -780,7 +900,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       unsigned mcnt = 0;
       int mycl = -1, myit = 0;
       if (sl < ncols) {
-        myit = S.sitem[sl];
+        myit = max(static_cast<int>(S.sitem[sl]), 0);
         mycl = S.scl[sl];
       }
       const bool mact = __ballot(mycl >= 0) != 0ull;  // wave-uniform: any running centre
@@ -793,9 +913,9 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         idx_issue<DP>(a, idx, RT, wave, lane, nI);
         dma_wait();
       }
-      unsigned pre[NS];  // E-step operands of tile t-1 (loaded in iteration t-1)
+      unsigned pre[NSS];  // closest distances of the seeding steps of tile t-1 (loaded in t-1)
 #pragma unroll
-      for (int i = 0; i < NS; ++i) pre[i] = 0;
+      for (int i = 0; i < NSS; ++i) pre[i] = 0;
 #ifdef CC_KM_STAMPS
       unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -810,33 +930,55 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         // tile t+2; E-step operands of tile t (consumed next iteration)
         if (t + 1 < T) tile_dma<DP>(a, nI, ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * 64, wave, lane);
         if (t + 2 < T) idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
-        unsigned npre[NS];
-        estep_prefetch(a, S, t, T, nitems, tidl, glab, dbuf, T1, npre);
+        unsigned npre[NSS];
+        estep_prefetch(a, S, t, T, tidl, dbuf, T1, npre);
         KM_STAMP(s1);
+        // Stagger: waves w and w+4 share a SIMD; w+4 runs its E-step (VALU) first so that one
+        // of the pair issues MFMAs while the other works on the vector pipe.
+        __builtin_amdgcn_sched_barrier(0);  // phases do not interleave: bounded working sets
+        if (wave >= 4) estep<DP>(a, S, t, T, tidl, Dt, Ls, XN, glab, dbuf, T1, pre, lw, nl, es);
+        __builtin_amdgcn_sched_barrier(0);
         // distances of tile t (MFMA) -> D[t & 1]
         if (tact && t < T) {
           const char* xs = ring + (t % NRING) * LY::SLOT;
           v16f acc = {};
+          int lro = lr;
+          asm volatile("" : "+v"(lro));  // recompute the swizzled offsets (cheap) rather than hold 8
+          // B operands one k-step ahead of the MFMAs (bounded: 16 VGPRs in flight)
+          h8 bh = *reinterpret_cast<const h8*>(xs + xoff<DP>(lro, hh));
+          h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + xoff<DP>(lro, hh));
 #pragma unroll
           for (int s = 0; s < DP / 16; ++s) {
-            const int off = xoff<DP>(lr, 2 * s + hh);
-            const h8 bh = *reinterpret_cast<const h8*>(xs + off);
-            const h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
+            h8 nh = bh, nl = bl;
+            if (s + 1 < DP / 16) {
+              const int off = xoff<DP>(lro, 2 * (s + 1) + hh);
+              nh = *reinterpret_cast<const h8*>(xs + off);
+              nl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
+            }
             acc = mfma16(ah[s], bl, acc);
             acc = mfma16(al[s], bh, acc);
             acc = mfma16(ah[s], bh, acc);
-            if (s & 1) __builtin_amdgcn_sched_barrier(0);  // bound the B operands in flight
+            __builtin_amdgcn_sched_barrier(0);
+            bh = nh;
+            bl = nl;
           }
           float* drow = Dt + (t & 1) * (RT * DSD) + lr * DSD + 32 * ct + 4 * hh;
           const float* cn = S.cnorm + 32 * ct + 4 * hh;
 #pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int i = (v & 3) + 8 * (v >> 2);
-            drow[i] = cn[i] - a.dscale * acc[v];
+          for (int g = 0; g < 4; ++g) {  // slots 8g + 4hh .. +3 of the tile: one b128 store
+            const float4 c4 = *reinterpret_cast<const float4*>(cn + 8 * g);
+            float4 d;
+            d.x = c4.x - a.dscale * acc[4 * g];
+            d.y = c4.y - a.dscale * acc[4 * g + 1];
+            d.z = c4.z - a.dscale * acc[4 * g + 2];
+            d.w = c4.w - a.dscale * acc[4 * g + 3];
+            *reinterpret_cast<float4*>(drow + 8 * g) = d;
           }
         }
         KM_STAMP(s2);
-        estep<DP>(a, S, t, T, nitems, tidl, Dt, Ls, XN, glab, dbuf, tsum, T1, pre, es);
+        __builtin_amdgcn_sched_barrier(0);
+        if (wave < 4) estep<DP>(a, S, t, T, tidl, Dt, Ls, XN, glab, dbuf, T1, pre, lw, nl, es);
+        __builtin_amdgcn_sched_barrier(0);
         KM_STAMP(s3);
         // M-step of tile t-2 (one-hot x X on f16 MFMA; counts by popcount)
         if (mact && t >= 2) {
@@ -879,10 +1021,15 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           }
         }
         KM_STAMP(s4);
-        dma_wait();  // tile t+1, the E-step operands and this iteration's stores have landed
+        // tile t+1 and the E-step operands have landed (this iteration's stores may still be
+        // in flight: one per Lloyd step, two per seeding step, issued after every load)
+        if (t >= 1 && t * RT <= m)  // tile t-1 full: every step issued its store instructions
+          dma_wait_leaving(__builtin_amdgcn_readfirstlane(S.nlw[wave]) + 2 * __builtin_amdgcn_readfirstlane(S.nsw[wave]));
+        else
+          dma_wait();
         KM_STAMP(s5);
 #pragma unroll
-        for (int i = 0; i < NS; ++i) pre[i] = npre[i];
+        for (int i = 0; i < NSS; ++i) pre[i] = npre[i];
         __syncthreads();
         KM_STAMP(s6);
         KM_ACC(0, s0, s1);
@@ -896,7 +1043,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       if (blockIdx.x == 0 && lane == 0 && a.stats)
         for (int k = 0; k < 7; ++k) atomicAdd(&a.stats[8 + 8 * wave + k], st_acc[k]);
 #endif
-      estep_finish(S, nitems, tid, es);
+      estep_finish(S, tid, es);
       // sums -> Sm (aliases the ring and D: every reader passed the last barrier); counts
       if (mact) {
 #pragma unroll
@@ -958,8 +1105,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           if (!S.need_sel[p]) continue;
           if ((j++ % NW) != wave) continue;
           const int ss = S.sslot[p];
-          kpp_select(a, S, p, dbuf + (static_cast<size_t>(ss) * T1 + S.cs[p]) * m,
-                     tsum + (static_cast<size_t>(ss) * a.Tws + S.sbest[p]) * T, lane);
+          kpp_select(a, S, p, dbuf + (static_cast<size_t>(ss) * T1 + S.cs[p]) * a.lsm, lane);
         }
       }
       // initial centres of problems leaving seeding: the chosen rows (exact f32)
@@ -972,6 +1118,28 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         }
         if (tid < K) cenn[S.cenoff[p] + tid] = row_sq(a.X + static_cast<size_t>(idx[cpos[p * a.Kws + tid]]) * DP, a.dreal);
       }
+
+      // ---- labels changed? (RUN items): compare this sweep's label buffer with the previous
+      // one, 16 B per thread and load; then this sweep's buffer becomes the current one
+      for (int it = 0; it < nitems; ++it) {
+        if (S.ikind[it] < IK_RUN) continue;
+        const int p = S.iprob[it];
+        bool diff = false;
+        if (S.ikind[it] == IK_RUN) {
+          const uint4* cur = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + 1 - S.lcur[p]) * a.lsm);
+          const uint4* old = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm);
+          for (int e = tid; e < (m + 15) / 16; e += NT) {
+            const uint4 x = cur[e], y = old[e];
+            diff |= (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
+          }
+        }
+        const int any = __syncthreads_or(diff);
+        if (tid == 0) {
+          S.ichanged[it] = any != 0;
+          S.lcur[p] = static_cast<unsigned char>(1 - S.lcur[p]);
+        }
+      }
+      __syncthreads();
 
       // ---- Lloyd M-step completion (RUN items) ------------------------------------
       if (tid == 0) {
@@ -992,7 +1160,8 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           if (S.ikind[it] != IK_RUN) continue;
           const int p = S.iprob[it];
           if (S.nempty[p] == 0) continue;
-          relocate<DP>(a, idx, p, S.ioff[it], cen, Sm, S, glab, rdist, tid);
+          relocate<DP>(a, idx, p, S.ioff[it], cen, Sm, S, glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm,
+                       rdist, tid);
           __syncthreads();
         }
       }
@@ -1010,7 +1179,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       for (int e = tid; e < ncols * DP; e += NT) {
         const int sl = e / DP, d = e - sl * DP;
         const int it = S.sitem[sl];
-        if (S.ikind[it] != IK_RUN || S.cnt[sl] != 0) continue;
+        if (it < 0 || S.ikind[it] != IK_RUN || S.cnt[sl] != 0) continue;
         const int p = S.iprob[it], off = S.ioff[it];
         if (sl - off > S.amax[p]) continue;
         Sm[sl * DP + d] = Sm[(off + S.amax[p]) * DP + d];
@@ -1018,7 +1187,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       __syncthreads();
       for (int e = tid; e < ncols * DP; e += NT) {
         const int sl = e / DP;
-        if (S.ikind[S.sitem[sl]] != IK_RUN) continue;
+        if (S.sitem[sl] < 0 || S.ikind[S.sitem[sl]] != IK_RUN) continue;
         const unsigned cn = S.cnt[sl];
         if (cn > 0) {
           const float alpha = static_cast<float>(1.0 / static_cast<double>(static_cast<float>(cn)));
@@ -1029,14 +1198,14 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       for (int e = tid; e < ncols * DP; e += NT) {
         const int sl = e / DP, d = e - sl * DP;
         const int it = S.sitem[sl];
-        if (S.ikind[it] != IK_RUN || S.cnt[sl] != 0) continue;
+        if (it < 0 || S.ikind[it] != IK_RUN || S.cnt[sl] != 0) continue;
         const int p = S.iprob[it], off = S.ioff[it];
         if (sl - off < S.amax[p]) continue;
         Sm[sl * DP + d] = Sm[(off + S.amax[p]) * DP + d];
       }
       __syncthreads();
       // centre shifts (sklearn _euclidean_dense_dense, 4-way unrolled f32)
-      if (tid < ncols && S.ikind[S.sitem[tid]] == IK_RUN) {
+      if (tid < ncols && S.sitem[tid] >= 0 && S.ikind[S.sitem[tid]] == IK_RUN) {
         const int sl = tid;
         const int it = S.sitem[sl];
         const int p = S.iprob[it];
@@ -1079,14 +1248,14 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       for (int e = tid; e < ncols * DP; e += NT) {
         const int sl = e / DP, d = e - sl * DP;
         const int it = S.sitem[sl];
-        if (S.ikind[it] != IK_RUN) continue;
+        if (it < 0 || S.ikind[it] != IK_RUN) continue;
         const int p = S.iprob[it];
         if (S.st[p] == ST_DONE) continue;
         cen[(S.cenoff[p] + (sl - S.ioff[it])) * DP + d] = Sm[e];
       }
       if (tid < ncols) {
         const int it = S.sitem[tid];
-        if (S.ikind[it] == IK_RUN) {
+        if (it >= 0 && S.ikind[it] == IK_RUN) {
           const int p = S.iprob[it];
           if (S.st[p] != ST_DONE) cenn[S.cenoff[p] + (tid - S.ioff[it])] = row_sq(Sm + tid * DP, a.dreal);
         }
@@ -1108,8 +1277,8 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         if (tid <= KMAX) S.map[tid] = -1;
         if (tid == 0) S.flag = 0;
         __syncthreads();
-        const uint8_t* l1 = glab + static_cast<size_t>(p) * a.lsm;
-        const uint8_t* l2 = glab + static_cast<size_t>(best) * a.lsm;
+        const uint8_t* l1 = glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm;
+        const uint8_t* l2 = glab + static_cast<size_t>(2 * best + S.lcur[best]) * a.lsm;
         for (int r = tid; r < m; r += NT) S.map[l1[r]] = l2[r];
         __syncthreads();
         bool bad = false;
@@ -1120,7 +1289,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         __syncthreads();
       }
       const int kidx = S.kidx[p0];
-      const uint8_t* lb = glab + static_cast<size_t>(best) * a.lsm;
+      const uint8_t* lb = glab + static_cast<size_t>(2 * best + S.lcur[best]) * a.lsm;
       uint8_t* out = a.labels_out + static_cast<size_t>(kidx) * a.n * a.ldl + h;
       for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = lb[r];
       if (tid == 0) {
@@ -1156,7 +1325,7 @@ int local_trials(int K) { return 2 + static_cast<int>(std::log(static_cast<doubl
 
 struct WsLayout {
   int Pws = 0, Cws = 0, Kws = 0, Tws = 0;
-  size_t off_cen = 0, off_cenn = 0, off_cpos = 0, off_dbuf = 0, off_tsum = 0, off_rdist = 0, per_wg = 0;
+  size_t off_cen = 0, off_cenn = 0, off_cpos = 0, off_dbuf = 0, off_rdist = 0, per_wg = 0;
 };
 
 constexpr size_t WS_HEADER = 256;  // the work counter
@@ -1174,14 +1343,12 @@ WsLayout ws_layout(int m, int dpad, const int32_t* units, int nU, int seedmax) {
     }
     L.Cws = std::max(L.Cws, cols);
   }
-  const int T = (m + RT - 1) / RT;
   auto al = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
-  L.off_cen = al(static_cast<size_t>(L.Pws) * ((m + 63) & ~63));
+  L.off_cen = al(static_cast<size_t>(2 * L.Pws) * ((m + 63) & ~63));
   L.off_cenn = L.off_cen + al(static_cast<size_t>(L.Cws) * dpad * sizeof(float));
   L.off_cpos = L.off_cenn + al(static_cast<size_t>(L.Cws) * sizeof(float));
   L.off_dbuf = L.off_cpos + al(static_cast<size_t>(L.Pws) * L.Kws * sizeof(int32_t));
-  L.off_tsum = L.off_dbuf + al(static_cast<size_t>(seedmax) * (L.Tws + 1) * m * sizeof(float));
-  L.off_rdist = L.off_tsum + al(static_cast<size_t>(seedmax) * L.Tws * T * sizeof(double));
+  L.off_rdist = L.off_dbuf + al(static_cast<size_t>(seedmax) * (L.Tws + 1) * ((m + 63) & ~63) * sizeof(float));
   L.per_wg = L.off_rdist + al(static_cast<size_t>(m) * sizeof(float));
   return L;
 }
@@ -1368,7 +1535,6 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
   a.off_cenn = L.off_cenn;
   a.off_cpos = L.off_cpos;
   a.off_dbuf = L.off_dbuf;
-  a.off_tsum = L.off_tsum;
   a.off_rdist = L.off_rdist;
   a.Pws = L.Pws;
   a.Kws = L.Kws;
