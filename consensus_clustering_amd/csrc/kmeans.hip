@@ -940,6 +940,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         // distances of tile t (MFMA) -> D[t & 1]
         if (tact && t < T) {
+          __builtin_amdgcn_s_setprio(1);  // MFMA-dense block first in the SIMD arbiter
           const char* xs = ring + (t % NRING) * LY::SLOT;
           v16f acc = {};
           int lro = lr;
@@ -974,6 +975,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
             d.w = c4.w - a.dscale * acc[4 * g + 3];
             *reinterpret_cast<float4*>(drow + 8 * g) = d;
           }
+          __builtin_amdgcn_s_setprio(0);
         }
         KM_STAMP(s2);
         __builtin_amdgcn_sched_barrier(0);
