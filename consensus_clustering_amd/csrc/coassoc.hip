@@ -139,6 +139,35 @@ __device__ __forceinline__ void expand(const uint32_t (&w)[32], uint32_t (&o)[32
   }
 }
 
+// Dwords 8 kc .. 8 kc + 7 of expand() (virtual k = 32 kc .. 32 kc + 31).
+template <int KP>
+__device__ __forceinline__ void expand_chunk(const uint32_t (&w)[32], int kc, uint32_t (&o)[8]) {
+  if constexpr (KP == 1) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (~w[8 * kc + q] >> 7) & 0x01010101u;  // byte != 0xFF
+  } else if constexpr (KP == 2) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const uint32_t x = w[4 * kc + p];
+      const uint32_t is0 = ~x & 0x01010101u;               // label == 0
+      const uint32_t is1 = x & ~(x >> 1) & 0x01010101u;    // label == 1 (0xFF excluded)
+      o[2 * p + 0] = spread01(is0 & 0x101u) | (spread01(is1 & 0x101u) << 8);
+      o[2 * p + 1] = spread01((is0 >> 16) & 0x101u) | (spread01((is1 >> 16) & 0x101u) << 8);
+    }
+  } else {
+    constexpr int LOG = (KP == 4) ? 2 : (KP == 8) ? 3 : (KP == 16) ? 4 : (KP == 32) ? 5
+                      : (KP == 64) ? 6 : 7;
+#pragma unroll
+    for (int qq = 0; qq < 8; ++qq) {
+      const int k0 = 4 * (8 * kc + qq);
+      const int h = k0 >> LOG;
+      const uint32_t cq = static_cast<uint32_t>((k0 & (KP - 1)) >> 2);
+      const uint32_t lab = (w[h >> 2] >> (8 * (h & 3))) & 0xFFu;
+      o[qq] = ((lab >> 2) == cq) ? (1u << ((lab & 3u) << 3)) : 0u;
+    }
+  }
+}
+
 template <int KP>
 __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     const uint8_t* __restrict__ labels, int n, int ldl, int Hpad, int64_t tile_begin,
@@ -174,9 +203,21 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = v16i{};
 
-  uint32_t w[32], o[32];
+  // Label prefetch depth: two steps ahead for the co-association kernels (<= 16 label bytes
+  // per row and step); the co-sampling kernel (128 bytes per row and step) loads one step
+  // ahead into a single buffer and expands after the MFMAs (its registers would spill).
+  constexpr bool PF2 = KP > 1;
+  constexpr int NWD = (HS + 3) / 4;
+  uint32_t w[32], wn[PF2 ? NWD : 1], o[32];
   load_labels<KP>(rowp, evalid, w);
   expand<KP>(w, o);
+  if constexpr (PF2) {
+    load_labels<KP>(rowp + (nsteps > 1 ? HS : 0), evalid, w);  // step 1
+    uint32_t t32[32];
+    load_labels<KP>(rowp + (nsteps > 2 ? 2 * HS : 0), evalid, t32);  // step 2
+#pragma unroll
+    for (int q = 0; q < NWD; ++q) wn[q] = t32[q];
+  }
 #pragma unroll
   for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
@@ -188,8 +229,10 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
 
   for (int s = 0; s < nsteps; ++s) {
     const bool more = (s + 1) < nsteps;
-    if (more) load_labels<KP>(rowp + (s + 1) * HS, evalid, w);
     const char* rb = lds + (s & 1) * BUF;
+    char* wb = wbase + ((s + 1) & 1) * BUF;
+    if constexpr (!PF2)
+      if (more) load_labels<KP>(rowp + (s + 1) * HS, evalid, w);
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       v4i a[4], b[2];
@@ -205,10 +248,30 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
 #pragma unroll
         for (int nj = 0; nj < 2; ++nj)
           acc[mi][nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[nj], acc[mi][nj], 0, 0, 0);
+      if constexpr (PF2) {
+        // one-hot expansion of step s+1 (labels prefetched two steps ahead) interleaved with
+        // this step's MFMAs: chunk kc's 8 dwords are expanded and stored right after chunk
+        // kc's MFMAs issue, so the vector work runs in the MFMA shadows
+        uint32_t oc[8];
+        expand_chunk<KP>(w, kc, oc);
+        if (more) {
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+            *reinterpret_cast<uint4*>(wb + kc * FRAG + g * 512) =
+                make_uint4(oc[g * 4 + 0], oc[g * 4 + 1], oc[g * 4 + 2], oc[g * 4 + 3]);
+        }
+      }
     }
-    if (more) {
+    if constexpr (PF2) {
+      // rotate the label prefetch: w <- step s+2, wn <- step s+3 (clamped re-reads at the end)
+#pragma unroll
+      for (int q = 0; q < NWD; ++q) w[q] = wn[q];
+      uint32_t t32[32];
+      load_labels<KP>(rowp + ((s + 3) < nsteps ? s + 3 : s) * HS, evalid, t32);
+#pragma unroll
+      for (int q = 0; q < NWD; ++q) wn[q] = t32[q];
+    } else if (more) {
       expand<KP>(w, o);
-      char* wb = wbase + ((s + 1) & 1) * BUF;
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
