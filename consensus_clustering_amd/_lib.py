@@ -37,6 +37,10 @@ SIGNATURES = {
                                    _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_int, _c_int,
                                    _c_dbl, _vp, _c_int, _vp, _vp, _c_int, _vp, _vp, _vp, _vp,
                                    _c_sz, _c_int, _c_int, _vp]),
+    "cc_kmeans_wide_workspace_bytes": (_c_sz, [_c_int, _c_int, _vp, _c_int, _c_int, _c_int]),
+    "cc_kmeans_wide": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int,
+                                _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_dbl, _vp, _c_int,
+                                _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_sz, _c_int, _vp]),
 }
 
 _lock = threading.Lock()

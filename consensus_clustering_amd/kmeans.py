@@ -23,6 +23,17 @@ USTRIDE = 1 + 4 * 64   # CC_KM_USTRIDE
 DPADS = (32, 64, 128)
 
 
+def dpad_for(d: int) -> int:
+    """Feature padding: 32/64/128 for the on-chip engine (cc_kmeans_batched), a multiple of 32
+    for the wide-row path (cc_kmeans_wide, d > 128)."""
+    if d <= 0:
+        raise ValueError("X must have at least one feature")
+    for p in DPADS:
+        if d <= p:
+            return p
+    return (d + 31) // 32 * 32
+
+
 def local_trials(K: int) -> int:
     return 2 + int(np.log(K))
 
@@ -94,9 +105,7 @@ def prepare_rows(X, device):
     so one global centring serves every resample.  Returns (Xd, xnorm, dpad, Xhl, e).
     """
     n, d = X.shape
-    dpad = next((p for p in DPADS if d <= p), None)
-    if dpad is None:
-        raise _lib.CCMIError(f"batched k-means supports d <= {DPADS[-1]} in this build (got d={d})")
+    dpad = dpad_for(d)
     Xt = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X))
     Xt = Xt.to(device)
     mean = Xt.to(torch.float64).mean(dim=0).to(torch.float32)
@@ -113,7 +122,7 @@ class BatchedKMeans:
     """All (h, K, init) k-means problems of a consensus fit, on one device."""
 
     def __init__(self, Ks, n_init=3, max_iter=300, tol=1e-4, random_state=0,
-                 workspace_budget=8 << 30, seedmax=16):
+                 workspace_budget=8 << 30, seedmax=16, wide_budget=48 << 30):
         self.Ks = [int(k) for k in Ks]
         self.n_init = int(n_init)
         self.max_iter = int(max_iter)
@@ -121,6 +130,7 @@ class BatchedKMeans:
         self.seed = int(random_state)
         self.workspace_budget = int(workspace_budget)
         self.seedmax = int(seedmax)
+        self.wide_budget = int(wide_budget)
         self.stats = None
         self.units = None
 
@@ -136,6 +146,9 @@ class BatchedKMeans:
         self.stats = torch.zeros(128, dtype=torch.int64, device=dev)  # [0:8] counters, rest: diagnostics
         if nh <= 0:
             return labels_nh
+        if Xd.shape[1] > DPADS[-1]:
+            return self._run_wide(Xd, xnorm, dreal, idx_d, n, H, m, h_begin, h_end, labels_nh,
+                                  weight_dtype, inertia, n_iter, Xhl, scale_exp)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         n_sub = choose_subsets(nh, len(self.Ks), cus)
         u_h = plan(self.Ks, self.n_init, n_sub)
@@ -161,4 +174,43 @@ class BatchedKMeans:
                       labels_nh.data_ptr(), ldl, _lib.ptr(inertia), _lib.ptr(n_iter),
                       self.stats.data_ptr(), ws.data_ptr(), ws.numel(), grid, seedmax,
                       engine.stream_ptr(dev))
+        return labels_nh
+
+    def _run_wide(self, Xd, xnorm, dreal, idx_d, n, H, m, h_begin, h_end, labels_nh, weight_dtype,
+                  inertia, n_iter, Xhl, scale_exp):
+        """d > 128: cc_kmeans_wide over batches of resamples sized to the workspace budget,
+        at most 64 (K, init) problems per call."""
+        dev = Xd.device
+        lib = _lib.load()
+        dpad = Xd.shape[1]
+        nh = h_end - h_begin
+        per_call = max(1, 64 // self.n_init)
+        free = torch.cuda.mem_get_info(dev)[0]
+        budget = min(self.wide_budget, int(0.6 * free))
+        ldl = labels_nh.stride(1)
+        for k0 in range(0, len(self.Ks), per_call):
+            Ks = self.Ks[k0:k0 + per_call]
+            Ks_np = np.ascontiguousarray(np.asarray(Ks, dtype=np.int32))
+            ws1 = lib.cc_kmeans_wide_workspace_bytes(m, dpad, Ks_np.ctypes.data, len(Ks),
+                                                     self.n_init, 1)
+            ws2 = lib.cc_kmeans_wide_workspace_bytes(m, dpad, Ks_np.ctypes.data, len(Ks),
+                                                     self.n_init, 2)
+            if ws1 == 0:
+                _lib.check(-1, "cc_kmeans_wide_workspace_bytes")
+            per = ws2 - ws1
+            batch = int(max(1, min(nh, (budget - (ws1 - per)) // per)))
+            ws = torch.empty(ws1 + per * (batch - 1), dtype=torch.uint8, device=dev)
+            u, pos, stride = kpp_tables(Ks, self.n_init, self.seed, m, weight_dtype)
+            u_d = torch.from_numpy(u).to(dev)
+            pos_d = torch.from_numpy(pos).to(dev)
+            with engine.timed("cc_kmeans_wide"):
+                _lib.call("cc_kmeans_wide", Xd.data_ptr(), Xhl.data_ptr(), xnorm.data_ptr(), n,
+                          int(dreal), dpad, int(scale_exp), idx_d.data_ptr(), H, m, h_begin, h_end,
+                          Ks_np.ctypes.data, len(Ks), self.n_init, self.max_iter, self.tol,
+                          u_d.data_ptr(), stride, pos_d.data_ptr(), labels_nh[k0].data_ptr(), ldl,
+                          None if inertia is None else inertia[k0].data_ptr(),
+                          None if n_iter is None else n_iter[k0].data_ptr(),
+                          self.stats.data_ptr(), ws.data_ptr(), ws.numel(), batch,
+                          engine.stream_ptr(dev))
+            del ws
         return labels_nh

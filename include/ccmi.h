@@ -19,6 +19,7 @@
  *   cc_kmeans_plan        packing of the (K, init) problems of one resample into units
  *   cc_split_f16          f16 hi/lo operand image of the rows for the k-means MFMAs
  *   cc_kmeans_batched     CC.py:282 clusterer.fit_predict for every (h, K) at once
+ *   cc_kmeans_wide        the same for wide rows (d > 128), as distance/centre GEMM rounds
  *                         (sklearn KMeans: k-means++ init, Lloyd, best of n_init)
  */
 #ifndef CCMI_H
@@ -142,6 +143,25 @@ int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const float* xnorm, i
                       int kpp_stride, const int32_t* kpp_pos, uint8_t* labels_nh, int ldl,
                       float* inertia, int32_t* n_iter, unsigned long long* stats,
                       void* workspace, size_t ws_bytes, int grid, int seedmax, void* stream);
+
+/* Wide rows (d > 128; BASELINE config 4, n = 5k x d = 20k): the same fits, decisions and
+ * outputs as cc_kmeans_batched (CC.py:282 for the default clusterer), organised as ROUNDS
+ * over a batch of `batch` resamples: per round a distance-GEMM launch fused with the
+ * E-step, a centre-sum GEMM launch and a per-resample bookkeeping launch, until every
+ * problem is done.  The call is synchronous with respect to the host (it reads one counter
+ * per round to stop).  Ks [nK] host array (nK * n_init <= CC_KM_PMAX per call); dpad any
+ * multiple of 32 >= dreal; other arguments as cc_kmeans_batched; stats[4] counts
+ * resample-rounds and stats[5] 256-slot column tiles x rounds. */
+size_t cc_kmeans_wide_workspace_bytes(int m, int dpad, const int32_t* Ks, int nK, int n_init,
+                                      int batch);
+
+int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* xnorm, int n, int dreal,
+                   int dpad, int scale_exp, const int32_t* idx_hm, int H, int m, int h_begin,
+                   int h_end, const int32_t* Ks, int nK, int n_init, int max_iter,
+                   double tol_rel, const double* kpp_u, int kpp_stride, const int32_t* kpp_pos,
+                   uint8_t* labels_nh, int ldl, float* inertia, int32_t* n_iter,
+                   unsigned long long* stats, void* workspace, size_t ws_bytes, int batch,
+                   void* stream);
 
 #ifdef __cplusplus
 }

@@ -49,6 +49,8 @@ def run_gpu(X, Ks, H, frac, seed, n_init=3):
     (2000, 64, 4, [2, 3, 4, 7], 5),
     (1200, 128, 6, [3, 6, 10], 4),
     (29, 29, 3, [2, 3, 5], 5),
+    (1200, 300, 5, [2, 3, 5, 8], 4),     # wide rows: cc_kmeans_wide
+    (700, 2000, 4, [2, 4, 6], 3),
 ])
 def test_labels_match_sklearn(n, d, k_true, Ks, H):
     from threadpoolctl import threadpool_limits
@@ -105,3 +107,45 @@ def test_launch_split_is_invariant():
     bk.run(Xd, xn, d, idx_d, n, H, m, 5, H, L2, np.float32, **kw)
     torch.cuda.synchronize()
     assert torch.equal(L1, L2)
+
+
+def test_wide_batching_is_invariant():
+    """Wide rows: the resample batch size (workspace budget) and launch split change nothing."""
+    dev = engine.require_gpu()
+    X = blobs(900, 260, 4, seed=5)
+    n, d = X.shape
+    Ks, H, m = [2, 4, 7], 6, 720
+    idx = engine.resample_indices(13, n, m, 0, H)
+    idx_d = torch.from_numpy(idx).to(dev)
+    Xd, xn, dpad, Xhl, e = prepare_rows(X, dev)
+    assert dpad == 288
+    L1 = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
+    L2 = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
+    i1 = torch.zeros((len(Ks), H), dtype=torch.float32, device=dev)
+    i2 = torch.zeros_like(i1)
+    kw = dict(Xhl=Xhl, scale_exp=e)
+    BatchedKMeans(Ks, random_state=13).run(Xd, xn, d, idx_d, n, H, m, 0, H, L1, np.float32,
+                                           inertia=i1, **kw)
+    bk = BatchedKMeans(Ks, random_state=13, wide_budget=1)  # one resample per batch
+    bk.run(Xd, xn, d, idx_d, n, H, m, 0, 2, L2, np.float32, inertia=i2, **kw)
+    bk.run(Xd, xn, d, idx_d, n, H, m, 2, H, L2, np.float32, inertia=i2, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(L1, L2)
+    assert torch.equal(i1, i2)
+
+
+def test_wide_c4_shape():
+    """BASELINE config 4's row shape (n = 5k samples x d = 20k features, m = 4000) on two
+    resamples: labels identical to sklearn's for K <= the true number of blobs."""
+    from threadpoolctl import threadpool_limits
+
+    X = blobs(5000, 20000, 6, seed=4, std=4.0)
+    Ks, H, seed = [2, 4, 6], 2, 0
+    idx, labs, inert, nit, stats = run_gpu(X, Ks, H, 0.8, seed)
+    assert stats[0] > 0 and stats[2] > 0
+    with threadpool_limits(8):
+        for k, K in enumerate(Ks):
+            for h in range(H):
+                ref = O.kmeans_labels(X[idx[h]], K, seed, n_init=3)
+                assert np.array_equal(ref, labs[k, h]), (K, h, np.mean(ref == labs[k, h]))
+    assert np.all(np.isfinite(inert))
