@@ -36,9 +36,11 @@ METRIC = "consensus fit wall-time + resample-clusterings/sec, n=50k d=128, 1/2/4
 CONFIGS = {
     # BASELINE.json configs[2]: the metric's workload
     "c3": dict(n=50_000, d=128, k_true=8, Ks=list(range(2, 21)), H=1000, frac=0.8),
-    # BASELINE.json configs[1] / configs[4] (d <= 128 paths), for ad-hoc runs
+    # BASELINE.json configs[1] / configs[4], for ad-hoc runs
     "c2": dict(n=10_000, d=64, k_true=6, Ks=list(range(2, 16)), H=500, frac=0.8),
     "c5": dict(n=200_000, d=32, k_true=6, Ks=list(range(2, 11)), H=256, frac=0.8),
+    # BASELINE.json configs[3]: wide rows (cc_kmeans_wide)
+    "c4": dict(n=5_000, d=20_000, k_true=6, Ks=list(range(2, 13)), H=1000, frac=0.8),
     "smoke": dict(n=4_000, d=32, k_true=5, Ks=list(range(2, 8)), H=64, frac=0.8),
 }
 # MI355X_MICROARCH.md: f16/bf16 dense MFMA peak 256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz.  One
@@ -175,7 +177,8 @@ def main():
     # max over ranks (wall) and sums over ranks (work, kernel time)
     vec = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     st = stats.to(torch.float64)
-    km_launch, km_ms = timers.get("cc_kmeans_batched", (0, 0.0))
+    km_kernel = "cc_kmeans_batched" if cfg["d"] <= 128 else "cc_kmeans_wide"
+    km_launch, km_ms = timers.get(km_kernel, (0, 0.0))
     ktime = torch.tensor([km_ms, float(km_launch)], dtype=torch.float64, device=dev)
     if world > 1:
         tdist.all_reduce(vec, op=tdist.ReduceOp.MAX)
@@ -210,7 +213,7 @@ def main():
                        "n": cfg["n"], "d": d, "K_range": [cfg["Ks"][0], cfg["Ks"][-1]],
                        "H": cfg["H"], "parallelism": f"resamples+triangle sharded over {world} GPU(s)"},
             "roofline": {
-                "kernel": "cc_kmeans_batched",
+                "kernel": km_kernel,
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": KMEANS_PEAK_TF,

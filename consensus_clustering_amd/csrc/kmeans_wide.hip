@@ -118,7 +118,7 @@ struct WArgs {
   unsigned long long* stats;
   int* active;             // scheduled column tiles of the next round (summed by P)
   uint8_t* ws;
-  size_t ws_per, off_tiles, off_part, off_glab, off_dbuf, off_cpos, off_cen, off_cenhl, off_cenn, off_rdist;
+  size_t ws_per, off_tolp, off_tiles, off_part, off_glab, off_dbuf, off_cpos, off_cen, off_cenhl, off_cenn, off_rdist;
 };
 
 struct RP {  // one resample's workspace
@@ -237,38 +237,48 @@ __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
   // loaders: A = slot tid>>1, plane tid&1 (64 B / stage); B = row tid>>2, plane (tid>>1)&1,
   // 32-B half tid&1
   const int sa = tid >> 1, pa = tid & 1;
-  const uint16_t* asrc = nullptr;
+  // every lane loads (no divergent loads: the compiler then counts vmcnt exactly); dummy and
+  // unused slots read row s_gidx[0]: a dummy's distance is +inf whatever its A operand
+  const uint16_t* asrc;
   {
     const int sr = s_srow[sa];
     if (sr >= 0) asrc = a.Xhl + (static_cast<size_t>(sr) * 2 + pa) * dpad;
     else if (sr != INT_MIN) asrc = R.cenhl + (static_cast<size_t>(-sr - 1) * 2 + pa) * dpad;
+    else asrc = a.Xhl + (static_cast<size_t>(s_gidx[0]) * 2 + pa) * dpad;
   }
   const int rb = tid >> 2, pb = (tid >> 1) & 1, qb = tid & 1;
   const uint16_t* bsrc = a.Xhl + (static_cast<size_t>(s_gidx[rb]) * 2 + pb) * dpad + 16 * qb;
   const int aoff = pa * APL + sa * AP;
   const int boff = 2 * APL + pb * BPL + rb * AP + 32 * qb;
-  uint4 ra[4], rbv[2];
-  auto gload = [&](int s) {
-    if (asrc) {
-      const uint4* p = reinterpret_cast<const uint4*>(asrc + KC * s);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) ra[q] = p[q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) ra[q] = make_uint4(0, 0, 0, 0);
-    }
-    const uint4* p = reinterpret_cast<const uint4*>(bsrc + KC * s);
-    rbv[0] = p[0];
-    rbv[1] = p[1];
+  // three stages of loads in flight: stage t lives in register set t % 3 from its issue (two
+  // stages before it is stored to LDS) until its store
+  // register sets are passed by value with named fields (an address-taken or array-member set
+  // is put in scratch, and every copy of a set with loads in flight waits for them)
+  struct ESet {
+    uint4 a0, a1, a2, a3, b0, b1;
   };
-  auto lstore = [&](int buf) {
+  auto gload = [&](int s) __attribute__((always_inline)) -> ESet {
+    ESet Rg;
+    const uint4* pa4 = reinterpret_cast<const uint4*>(asrc + KC * s);
+    Rg.a0 = pa4[0];
+    Rg.a1 = pa4[1];
+    Rg.a2 = pa4[2];
+    Rg.a3 = pa4[3];
+    const uint4* p = reinterpret_cast<const uint4*>(bsrc + KC * s);
+    Rg.b0 = p[0];
+    Rg.b1 = p[1];
+    return Rg;
+  };
+  auto lstore = [&](int buf, const ESet Rg) __attribute__((always_inline)) {
     char* base = sm + buf * STG;
     uint4* pA = reinterpret_cast<uint4*>(base + aoff);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) pA[q] = ra[q];
+    pA[0] = Rg.a0;
+    pA[1] = Rg.a1;
+    pA[2] = Rg.a2;
+    pA[3] = Rg.a3;
     uint4* pB = reinterpret_cast<uint4*>(base + boff);
-    pB[0] = rbv[0];
-    pB[1] = rbv[1];
+    pB[0] = Rg.b0;
+    pB[1] = Rg.b1;
   };
 
   const int S = dpad / KC;
@@ -279,41 +289,59 @@ __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = v16f{};
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int s = 0; s < S; ++s) {
-    if (s + 1 < S) gload(s + 1);
-    if (wact) {
-      const char* base = sm + (s & 1) * STG;
+  auto compute = [&](int s) __attribute__((always_inline)) {
+    if (!wact) return;
+    const char* base = sm + (s & 1) * STG;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        h8 ah[2], al[2], bh[2], bl[2];
+    for (int ks = 0; ks < 2; ++ks) {
+      h8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int o = (64 * ws + 32 * i + lr) * AP + 32 * ks + 16 * hh;
-          ah[i] = *reinterpret_cast<const h8*>(base + o);
-          al[i] = *reinterpret_cast<const h8*>(base + APL + o);
-        }
+      for (int i = 0; i < 2; ++i) {
+        const int o = (64 * ws + 32 * i + lr) * AP + 32 * ks + 16 * hh;
+        ah[i] = *reinterpret_cast<const h8*>(base + o);
+        al[i] = *reinterpret_cast<const h8*>(base + APL + o);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int o = 2 * APL + (64 * wr + 32 * j + lr) * AP + 32 * ks + 16 * hh;
+        bh[j] = *reinterpret_cast<const h8*>(base + o);
+        bl[j] = *reinterpret_cast<const h8*>(base + BPL + o);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const int o = 2 * APL + (64 * wr + 32 * j + lr) * AP + 32 * ks + 16 * hh;
-          bh[j] = *reinterpret_cast<const h8*>(base + o);
-          bl[j] = *reinterpret_cast<const h8*>(base + BPL + o);
+          acc[i][j] = mfma16(ah[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma16(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma16(ah[i], bh[j], acc[i][j]);
         }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc[i][j] = mfma16(ah[i], bl[j], acc[i][j]);
-            acc[i][j] = mfma16(al[i], bh[j], acc[i][j]);
-            acc[i][j] = mfma16(ah[i], bh[j], acc[i][j]);
-          }
-      }
     }
-    if (s + 1 < S) lstore((s + 1) & 1);
+  };
+  ESet R0 = gload(0);
+  lstore(0, R0);
+  ESet R1 = gload(min(1, S - 1));
+  ESet R2 = gload(min(2, S - 1));
+  R0 = gload(min(3, S - 1));
+  __syncthreads();
+  // step s: compute stage s; store stage s+1 (set Rg) to the other buffer; reload Rg with s+4.
+  // Straight-line, every load unconditional (clamped stage index; the extra loads and stores
+  // are never read), so the waits count exactly two younger stages.
+  auto step = [&](int s, const ESet Rg) __attribute__((always_inline)) -> ESet {
+    compute(s);
+    lstore((s + 1) & 1, Rg);
+    __builtin_amdgcn_sched_barrier(0);
+    const ESet Rn = gload(min(s + 4, S - 1));
     __syncthreads();
+    return Rn;
+  };
+  int s = 0;
+  for (; s + 3 <= S; s += 3) {
+    R1 = step(s, R1);
+    R2 = step(s + 1, R2);
+    R0 = step(s + 2, R0);
   }
+  if (s < S) R1 = step(s, R1);
+  if (s + 1 < S) R2 = step(s + 1, R2);
 
   // distance tile D[row][slot] = |c|^2 - 2 x.c (aliases the stages: the loop ended on a barrier)
   float* D = reinterpret_cast<float*>(sm);
@@ -383,7 +411,7 @@ __global__ __launch_bounds__(NT, 1) void wide_mstep(WArgs a) {
   constexpr int PL = MRS * MP;  // one plane of a stage
   constexpr int STG = 2 * PL;
   __shared__ __attribute__((aligned(16))) char sm[2 * STG];
-  __shared__ __attribute__((aligned(16))) uint8_t Lb[2][IMW][MRS];
+  __shared__ __attribute__((aligned(16))) uint8_t Lb[2][IMW + 1][MRS];  // row IMW: sink of idle loaders
   __shared__ short s_scl[CWW], s_dst[CWW];
   __shared__ unsigned char s_item[CWW];
   __shared__ int s_ritem[IMW], s_lofs[IMW];
@@ -429,30 +457,37 @@ __global__ __launch_bounds__(NT, 1) void wide_mstep(WArgs a) {
   // loaders: X = row tid>>4, plane (tid>>3)&1, 32-feature piece tid&7 (64 B); labels = RUN item
   // tid>>1, 16-B half tid&1
   const int xr = tid >> 4, xp = (tid >> 3) & 1, xq = tid & 7;
-  const int f0 = dt * MDW + 32 * xq;
-  const bool xon = f0 < dpad;
+  // every lane loads (exact vmcnt counting): pieces past dpad re-read the last piece (their
+  // columns are never stored), idle label loaders read item 0's labels into the sink row
+  const int f0 = min(dt * MDW + 32 * xq, dpad - 32);
   const int xoffl = xp * PL + xr * MP + 64 * xq;
   const bool lon = tid < 2 * nr;
-  const uint8_t* lsrc = lon ? R.glab + s_lofs[tid >> 1] + 16 * (tid & 1) : nullptr;
-  uint8_t* ldst0 = lon ? &Lb[0][s_ritem[tid >> 1]][16 * (tid & 1)] : nullptr;
-  uint4 rx[4], rl = make_uint4(0, 0, 0, 0);
-  int gi = idx[min(xr, m - 1)];
-  auto gload = [&](int s) {
-    if (xon) {
-      const uint4* p = reinterpret_cast<const uint4*>(a.Xhl + (static_cast<size_t>(gi) * 2 + xp) * dpad + f0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) rx[q] = p[q];
-    }
-    if (lon) rl = *reinterpret_cast<const uint4*>(lsrc + MRS * s);
-    gi = idx[min((s + 1) * MRS + xr, m - 1)];  // next stage's row
+  const uint8_t* lsrc = R.glab + (lon ? s_lofs[tid >> 1] : 0) + 16 * (tid & 1);
+  uint8_t* ldst0 = &Lb[0][lon ? s_ritem[tid >> 1] : IMW][16 * (tid & 1)];
+  // a register set carries one stage's loads and the row index of the stage 3 later (by value:
+  // see wide_estep)
+  struct MSet {  // named fields: an array member makes the set a scratch object
+    uint4 x0, x1, x2, x3, l;
+    int gi;
   };
-  auto lstore = [&](int buf) {
-    if (xon) {
-      uint4* p = reinterpret_cast<uint4*>(sm + buf * STG + xoffl);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) p[q] = rx[q];
-    }
-    if (lon) *reinterpret_cast<uint4*>(ldst0 + buf * (IMW * MRS)) = rl;
+  auto gload = [&](int s, const MSet R) __attribute__((always_inline)) -> MSet {
+    MSet Rg;
+    const uint4* p = reinterpret_cast<const uint4*>(a.Xhl + (static_cast<size_t>(R.gi) * 2 + xp) * dpad + f0);
+    Rg.x0 = p[0];
+    Rg.x1 = p[1];
+    Rg.x2 = p[2];
+    Rg.x3 = p[3];
+    Rg.l = *reinterpret_cast<const uint4*>(lsrc + MRS * s);
+    Rg.gi = idx[min((s + 3) * MRS + xr, m - 1)];
+    return Rg;
+  };
+  auto lstore = [&](int buf, const MSet Rg) __attribute__((always_inline)) {
+    uint4* p = reinterpret_cast<uint4*>(sm + buf * STG + xoffl);
+    p[0] = Rg.x0;
+    p[1] = Rg.x1;
+    p[2] = Rg.x2;
+    p[3] = Rg.x3;
+    *reinterpret_cast<uint4*>(ldst0 + buf * ((IMW + 1) * MRS)) = Rg.l;
   };
 
   const int ws = wave & 3, wd = wave >> 2, lr = lane & 31, hh = lane >> 5;
@@ -473,52 +508,71 @@ __global__ __launch_bounds__(NT, 1) void wide_mstep(WArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = v16f{};
   const int S = (m + MRS - 1) / MRS;
   const int Gq = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int s = 0; s < S; ++s) {
-    if (s + 1 < S) gload(s + 1);
-    if (wact) {
-      const char* base = sm + (s & 1) * STG;
+  auto compute = [&](int s) __attribute__((always_inline)) {
+    if (!wact) return;
+    const char* base = sm + (s & 1) * STG;
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        h8 oh[2];
+    for (int ks = 0; ks < 2; ++ks) {
+      h8 oh[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const unsigned long long lab8 =
-              *reinterpret_cast<const unsigned long long*>(&Lb[s & 1][itm[i]][16 * ks + 8 * hh]);
-          u32x4 ohu;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
-            const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
-            ohu[j] = ((b0 == cl[i]) ? 0x3C00u : 0u) | ((b1 == cl[i]) ? 0x3C000000u : 0u);
-          }
-          oh[i] = __builtin_bit_cast(h8, ohu);
-        }
-        const int row0 = 16 * ks + 8 * (Gq >> 1) + q;
+      for (int i = 0; i < 2; ++i) {
+        const unsigned long long lab8 =
+            *reinterpret_cast<const unsigned long long*>(&Lb[s & 1][itm[i]][16 * ks + 8 * hh]);
+        u32x4 ohu;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (j >= nbd) break;
-          const int a0 = row0 * MP + 2 * (128 * wd + 32 * j + 16 * (Gq & 1) + 4 * pp);
-          const int a1 = a0 + 4 * MP;
-          const s4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + a0));
-          const s4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + a1));
-          const s4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + PL + a0));
-          const s4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + PL + a1));
-          const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
-          const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7));
+          const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
+          const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
+          ohu[j] = ((b0 == cl[i]) ? 0x3C00u : 0u) | ((b1 == cl[i]) ? 0x3C000000u : 0u);
+        }
+        oh[i] = __builtin_bit_cast(h8, ohu);
+      }
+      const int row0 = 16 * ks + 8 * (Gq >> 1) + q;
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            acc[i][j] = mfma16(oh[i], bl, acc[i][j]);
-            acc[i][j] = mfma16(oh[i], bh, acc[i][j]);
-          }
+      for (int j = 0; j < 4; ++j) {
+        if (j >= nbd) break;
+        const int a0 = row0 * MP + 2 * (128 * wd + 32 * j + 16 * (Gq & 1) + 4 * pp);
+        const int a1 = a0 + 4 * MP;
+        const s4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + a0));
+        const s4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + a1));
+        const s4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + PL + a0));
+        const s4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + PL + a1));
+        const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
+        const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          acc[i][j] = mfma16(oh[i], bl, acc[i][j]);
+          acc[i][j] = mfma16(oh[i], bh, acc[i][j]);
         }
       }
     }
-    if (s + 1 < S) lstore((s + 1) & 1);
+  };
+  MSet R0, R1, R2;
+  R0.gi = idx[min(xr, m - 1)];
+  R1.gi = idx[min(MRS + xr, m - 1)];
+  R2.gi = idx[min(2 * MRS + xr, m - 1)];
+  R0 = gload(0, R0);
+  lstore(0, R0);
+  R1 = gload(min(1, S - 1), R1);
+  R2 = gload(min(2, S - 1), R2);
+  R0 = gload(min(3, S - 1), R0);
+  __syncthreads();
+  auto step = [&](int s, const MSet Rg) __attribute__((always_inline)) -> MSet {
+    compute(s);
+    lstore((s + 1) & 1, Rg);
+    __builtin_amdgcn_sched_barrier(0);
+    const MSet Rn = gload(min(s + 4, S - 1), Rg);
     __syncthreads();
+    return Rn;
+  };
+  int s = 0;
+  for (; s + 3 <= S; s += 3) {
+    R1 = step(s, R1);
+    R2 = step(s + 1, R2);
+    R0 = step(s + 2, R0);
   }
+  if (s < S) R1 = step(s, R1);
+  if (s + 1 < S) R2 = step(s + 1, R2);
   if (wact) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -532,6 +586,48 @@ __global__ __launch_bounds__(NT, 1) void wide_mstep(WArgs a) {
           if (dst >= 0) R.cen[static_cast<size_t>(dst) * dpad + fw + 32 * j + lr] = acc[i][j][v] * a.inv_scale;
         }
       }
+  }
+}
+
+// ============================================================================================
+// tol pre-pass: sum over a 512-feature chunk of var(X_sub[:, f]) (f64, one pass, fixed order),
+// one workgroup per (resample, chunk); the init sums the chunks in order.
+// ============================================================================================
+__global__ __launch_bounds__(NT) void wide_tol(WArgs a) {
+  __shared__ double red[NW];
+  const int NTC = (a.dreal + NT - 1) / NT;
+  const int b = blockIdx.x / NTC, ch = blockIdx.x - b * NTC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int d = ch * NT + tid, m = a.m;
+  const int32_t* idx = a.idx + static_cast<size_t>(a.h0 + b) * m;
+  double v = 0.0;
+  if (d < a.dreal) {
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    const float* col = a.X + d;
+    int r = 0;
+    for (; r + 4 <= m; r += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double x = static_cast<double>(col[static_cast<size_t>(idx[r + u]) * a.dpad]);
+        s1[u] += x;
+        s2[u] += x * x;
+      }
+    }
+    for (; r < m; ++r) {
+      const double x = static_cast<double>(col[static_cast<size_t>(idx[r]) * a.dpad]);
+      s1[0] += x;
+      s2[0] += x * x;
+    }
+    const double mu = ((s1[0] + s1[1]) + (s1[2] + s1[3])) / m;
+    v = fmax(((s2[0] + s2[1]) + (s2[2] + s2[3])) / m - mu * mu, 0.0);
+  }
+  v = wave_sum(v);
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    for (int w = 0; w < NW; ++w) t += red[w];
+    reinterpret_cast<double*>(a.ws + static_cast<size_t>(b) * a.ws_per + a.off_tolp)[ch] = t;
   }
 }
 
@@ -821,24 +917,11 @@ __device__ void post_body(const WArgs& a, PS& L, bool init) {
       }
     }
     for (size_t e = tid; e < static_cast<size_t>(2 * a.P) * a.lsm; e += NT) R.glab[e] = 0xFF;
-    // tol = tol_rel * mean(var(X_sub, axis=0)) (sklearn _tolerance, :270-278), f64
-    double tv = 0.0;
-    for (int d = tid; d < a.dreal; d += NT) {
-      double s1 = 0.0, s2 = 0.0;
-      for (int r = 0; r < m; ++r) {
-        const double x = static_cast<double>(a.X[static_cast<size_t>(idx[r]) * dpad + d]);
-        s1 += x;
-        s2 += x * x;
-      }
-      const double mu = s1 / m;
-      tv += fmax(s2 / m - mu * mu, 0.0);
-    }
-    tv = wave_sum(tv);
-    if (lane == 0) L.red_v[wave] = tv;
-    __syncthreads();
+    // tol = tol_rel * mean(var(X_sub, axis=0)) (sklearn _tolerance, :270-278), from wide_tol
     if (tid == 0) {
+      const double* tp = reinterpret_cast<const double*>(a.ws + static_cast<size_t>(b) * a.ws_per + a.off_tolp);
       double tot = 0.0;
-      for (int w = 0; w < NW; ++w) tot += L.red_v[w];
+      for (int ch = 0; ch < (a.dreal + NT - 1) / NT; ++ch) tot += tp[ch];
       S.tol = static_cast<float>(static_cast<float>(tot / a.dreal) * a.tol_rel);
     }
     __syncthreads();
@@ -1177,7 +1260,7 @@ constexpr size_t HDR = 4096;  // active counter + problem table
 
 struct WL {
   int P = 0, Cn = 0, nct = 0, ndb = 0, kws = 0, RE = 0, DT = 0, lsm = 0;
-  size_t off_tiles = 0, off_part = 0, off_glab = 0, off_dbuf = 0, off_cpos = 0, off_cen = 0, off_cenhl = 0,
+  size_t off_tolp = 0, off_tiles = 0, off_part = 0, off_glab = 0, off_dbuf = 0, off_cpos = 0, off_cen = 0, off_cenhl = 0,
          off_cenn = 0, off_rdist = 0, per = 0;
 };
 
@@ -1215,6 +1298,8 @@ bool wide_layout(int m, int dpad, const int32_t* Ks, int nK, int n_init, WL& L) 
   L.lsm = (m + 63) & ~63;
   auto al = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
   size_t o = al(sizeof(WState));
+  L.off_tolp = o;
+  o += al(sizeof(double) * ((dpad + NT - 1) / NT));
   L.off_tiles = o;
   o += al(sizeof(WTile) * nct);
   L.off_part = o;
@@ -1335,6 +1420,7 @@ extern "C" int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* 
   a.active = active;
   a.ws = base + HDR;
   a.ws_per = L.per;
+  a.off_tolp = L.off_tolp;
   a.off_tiles = L.off_tiles;
   a.off_part = L.off_part;
   a.off_glab = L.off_glab;
@@ -1352,6 +1438,7 @@ extern "C" int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* 
     a.h0 = h0;
     a.nb = nb;
     if ((e = hipMemsetAsync(active, 0, sizeof(int), st)) != hipSuccess) return hip_fail("memset", e);
+    hipLaunchKernelGGL(wide_tol, dim3(nb * ((dreal + NT - 1) / NT)), dim3(NT), 0, st, a);
     hipLaunchKernelGGL(wide_init, dim3(nb), dim3(NT), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail("init launch", e);
     const int G = nb * L.nct;

@@ -23,6 +23,27 @@ USTRIDE = 1 + 4 * 64   # CC_KM_USTRIDE
 DPADS = (32, 64, 128)
 
 
+_WORKSPACE = {}
+
+
+def workspace(device, nbytes: int) -> torch.Tensor:
+    """Device scratch for the k-means launches, kept across fits: re-allocating tens of GB per
+    fit costs more than the fit (the caching allocator splits freed blocks for small tensors)."""
+    key = str(device)
+    t = _WORKSPACE.get(key)
+    if t is None or t.numel() < nbytes:
+        _WORKSPACE.pop(key, None)
+        del t
+        t = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+        _WORKSPACE[key] = t
+    return t[:int(nbytes)]
+
+
+def release_workspace():
+    """Drop the cached k-means workspace(s)."""
+    _WORKSPACE.clear()
+
+
 def dpad_for(d: int) -> int:
     """Feature padding: 32/64/128 for the on-chip engine (cc_kmeans_batched), a multiple of 32
     for the wide-row path (cc_kmeans_wide, d > 128)."""
@@ -122,7 +143,7 @@ class BatchedKMeans:
     """All (h, K, init) k-means problems of a consensus fit, on one device."""
 
     def __init__(self, Ks, n_init=3, max_iter=300, tol=1e-4, random_state=0,
-                 workspace_budget=8 << 30, seedmax=16, wide_budget=48 << 30):
+                 workspace_budget=8 << 30, seedmax=16, wide_budget=96 << 30):
         self.Ks = [int(k) for k in Ks]
         self.n_init = int(n_init)
         self.max_iter = int(max_iter)
@@ -164,7 +185,7 @@ class BatchedKMeans:
         grid = min(cus, nh * nU)
         while grid > 1 and per(grid) > self.workspace_budget:
             grid //= 2
-        ws = torch.empty(per(grid), dtype=torch.uint8, device=dev)
+        ws = workspace(dev, per(grid))
         ldl = labels_nh.stride(1)
         with engine.timed("cc_kmeans_batched"):
             _lib.call("cc_kmeans_batched", Xd.data_ptr(), Xhl.data_ptr(), xnorm.data_ptr(), n,
@@ -198,8 +219,9 @@ class BatchedKMeans:
             if ws1 == 0:
                 _lib.check(-1, "cc_kmeans_wide_workspace_bytes")
             per = ws2 - ws1
-            batch = int(max(1, min(nh, (budget - (ws1 - per)) // per)))
-            ws = torch.empty(ws1 + per * (batch - 1), dtype=torch.uint8, device=dev)
+            cap = int(max(1, min(nh, (budget - (ws1 - per)) // per)))
+            batch = -(-nh // -(-nh // cap))  # equal batches: one round-count tail per batch
+            ws = workspace(dev, ws1 + per * (batch - 1))
             u, pos, stride = kpp_tables(Ks, self.n_init, self.seed, m, weight_dtype)
             u_d = torch.from_numpy(u).to(dev)
             pos_d = torch.from_numpy(pos).to(dev)
@@ -212,5 +234,4 @@ class BatchedKMeans:
                           None if n_iter is None else n_iter[k0].data_ptr(),
                           self.stats.data_ptr(), ws.data_ptr(), ws.numel(), batch,
                           engine.stream_ptr(dev))
-            del ws
         return labels_nh
