@@ -18,14 +18,28 @@ Bit-exact for every W: integer counts, order-free reductions.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
 
+def _live() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def world() -> tuple:
-    """(rank, world_size) of the default process group, (0, 1) when not initialised."""
-    if dist.is_available() and dist.is_initialized():
+    """(rank, world_size) of the default process group, (0, 1) when not initialised.
+
+    ``CCMI_SIM_RANK=r/W`` (no process group) runs rank r's shard of a W-rank fit alone, with
+    the exchanges skipped: a one-GPU rehearsal of the per-rank critical path (timing only,
+    the results are partial)."""
+    if _live():
         return dist.get_rank(), dist.get_world_size()
+    sim = os.environ.get("CCMI_SIM_RANK")
+    if sim:
+        r, w = (int(v) for v in sim.split("/"))
+        return r, w
     return 0, 1
 
 
@@ -38,20 +52,17 @@ def shard(total: int, rank: int, world_size: int) -> tuple:
 
 def merge_labels(labels: torch.Tensor) -> torch.Tensor:
     """Assemble per-rank label matrices (0xFF where not owned) in place."""
-    _, W = world()
-    if W > 1:
+    if _live() and dist.get_world_size() > 1:
         dist.all_reduce(labels, op=dist.ReduceOp.MIN)
     return labels
 
 
 def sum_counts(t: torch.Tensor) -> torch.Tensor:
-    _, W = world()
-    if W > 1:
+    if _live() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
 
 
 def barrier():
-    _, W = world()
-    if W > 1:
+    if _live() and dist.get_world_size() > 1:
         dist.barrier()

@@ -14,6 +14,8 @@ the remaining doubles to the kernel.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -171,7 +173,7 @@ class BatchedKMeans:
             return self._run_wide(Xd, xnorm, dreal, idx_d, n, H, m, h_begin, h_end, labels_nh,
                                   weight_dtype, inertia, n_iter, Xhl, scale_exp)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        n_sub = choose_subsets(nh, len(self.Ks), cus)
+        n_sub = int(os.environ.get("CCMI_NSUB", 0)) or choose_subsets(nh, len(self.Ks), cus)
         u_h = plan(self.Ks, self.n_init, n_sub)
         self.units = u_h
         nU = u_h.shape[0]
