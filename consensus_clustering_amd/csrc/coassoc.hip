@@ -233,33 +233,48 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     char* wb = wbase + ((s + 1) & 1) * BUF;
     if constexpr (!PF2)
       if (more) load_labels<KP>(rowp + (s + 1) * HS, evalid, w);
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      v4i a[4], b[2];
+    // operand fragments double-buffered across the k-chunks: the reads of chunk kc+1 are in
+    // flight while chunk kc's MFMAs issue (only the first chunk's read latency is exposed)
+    v4i a[2][4], b[2][2];
+    auto frags = [&](int kc, v4i (&fa)[4], v4i (&fb)[2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
-        a[mi] = *reinterpret_cast<const v4i*>(rb + ((wr * 4 + mi) * KC + kc) * FRAG + lane * 16);
+        fa[mi] = *reinterpret_cast<const v4i*>(rb + ((wr * 4 + mi) * KC + kc) * FRAG + lane * 16);
 #pragma unroll
       for (int nj = 0; nj < 2; ++nj)
-        b[nj] = *reinterpret_cast<const v4i*>(rb + SIDE + ((wc * 2 + nj) * KC + kc) * FRAG +
-                                              lane * 16);
+        fb[nj] = *reinterpret_cast<const v4i*>(rb + SIDE + ((wc * 2 + nj) * KC + kc) * FRAG +
+                                               lane * 16);
+    };
+    frags(0, a[0], b[0]);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int cb = kc & 1;
+      if (kc + 1 < KC) frags(kc + 1, a[cb ^ 1], b[cb ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int nj = 0; nj < 2; ++nj)
-          acc[mi][nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], b[nj], acc[mi][nj], 0, 0, 0);
+          acc[mi][nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cb][mi], b[cb][nj], acc[mi][nj], 0, 0, 0);
       if constexpr (PF2) {
         // one-hot expansion of step s+1 (labels prefetched two steps ahead) interleaved with
         // this step's MFMAs: chunk kc's 8 dwords are expanded and stored right after chunk
         // kc's MFMAs issue, so the vector work runs in the MFMA shadows
+        // (the stores are unconditional: on the last step they land in the buffer nobody reads)
         uint32_t oc[8];
         expand_chunk<KP>(w, kc, oc);
-        if (more) {
 #pragma unroll
-          for (int g = 0; g < 2; ++g)
-            *reinterpret_cast<uint4*>(wb + kc * FRAG + g * 512) =
-                make_uint4(oc[g * 4 + 0], oc[g * 4 + 1], oc[g * 4 + 2], oc[g * 4 + 3]);
+        for (int g = 0; g < 2; ++g)
+          *reinterpret_cast<uint4*>(wb + kc * FRAG + g * 512) =
+              make_uint4(oc[g * 4 + 0], oc[g * 4 + 1], oc[g * 4 + 2], oc[g * 4 + 3]);
+        // issue order: each MFMA followed by a few expansion VALU ops, which then execute in
+        // that MFMA's 32-cycle shadow instead of after the whole MFMA block
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // up to 6 VALU
         }
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);    // the 2 LDS stores
       }
     }
     if constexpr (PF2) {
