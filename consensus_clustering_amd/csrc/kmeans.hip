@@ -506,9 +506,14 @@ __device__ void kpp_select(const KArgs& a, State& S, int p, const float* closest
 // Item words (LDS):
 //   iw0 = label buffer<<30 | kind<<24 | problem<<16 | K<<8 | slot offset
 //   iw1 = dbuf write slot<<11 | closest slot<<8 | trial<<5 | seeding slot
+// Per-thread inertia / potential partials of the wave's E-step steps: f32 over at most 32 tiles,
+// then flushed (f64 half-wave sum) into the item's f64 accumulator in LDS (S.iinert).  f32
+// partials keep 8 VGPRs instead of 16: with f64 partials the kernel spilled, and every spill
+// reload drained the LDS-DMA pipeline (vmcnt(0)).
 struct EState {
-  double iaccL[NLS], iaccS[NSS];
+  float iaccL[NLS], iaccS[NSS];
 };
+constexpr int FLUSH = 32;  // tiles per f32 partial
 
 __device__ __forceinline__ int iw_off(unsigned w) { return w & 0xFF; }
 __device__ __forceinline__ int iw_K(unsigned w) { return (w >> 8) & 0xFF; }
@@ -595,7 +600,7 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
     if (hh == 0) {
       if (eok) {
         glab[(static_cast<size_t>(2 * iw_prob(ww) + iw_buf(ww))) * a.lsm + erow] = static_cast<uint8_t>(lab);
-        es.iaccL[i] += static_cast<double>(xnr) + static_cast<double>(best);
+        es.iaccL[i] += xnr + best;
       }
       lsb[it * RT + ler] = eok ? static_cast<uint8_t>(lab) : 0xFF;
     }
@@ -612,23 +617,27 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
     const float dm = (iw_kind(ww) == IK_SEED) ? fminf(__uint_as_float(pre[i]), dist) : dist;
     if (eok && has) {
       dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 11) & 7)) * a.lsm + erow] = dm;
-      es.iaccS[i] += static_cast<double>(dm);
+      es.iaccS[i] += dm;
     }
   }
 }
 
-__device__ __forceinline__ void estep_finish(State& S, int tid, const EState& es) {
+// Add the f32 partials into the items' f64 accumulators (each item has exactly one
+// contributing half-wave, so lane 0 of it is the only writer) and restart them.
+__device__ __forceinline__ void estep_flush(State& S, int tid, EState& es) {
   const int er = tid & (RT - 1), hh = (tid >> 5) & 1, w = tid >> 6;
   const int nl = S.nlw[w], ns = S.nsw[w];
 #pragma unroll
   for (int i = 0; i < NLS; ++i) {
-    const double v = half_sum(es.iaccL[i]);
-    if (i < nl && er == 0 && hh == 0) S.iinert[S.lstep[w][i]] = v;
+    const double v = half_sum(static_cast<double>(es.iaccL[i]));
+    if (i < nl && er == 0 && hh == 0) S.iinert[S.lstep[w][i]] += v;
+    es.iaccL[i] = 0.f;
   }
 #pragma unroll
   for (int i = 0; i < NSS; ++i) {
-    const double v = half_sum(es.iaccS[i]);
-    if (i < ns && er == 0 && S.sstep[w][i][hh] != 0xFF) S.iinert[S.sstep[w][i][hh]] = v;
+    const double v = half_sum(static_cast<double>(es.iaccS[i]));
+    if (i < ns && er == 0 && S.sstep[w][i][hh] != 0xFF) S.iinert[S.sstep[w][i][hh]] += v;
+    es.iaccS[i] = 0.f;
   }
 }
 
@@ -875,7 +884,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       const int sl = 32 * ct + lr;
       EState es;
 #pragma unroll
-      for (int i = 0; i < NLS; ++i) es.iaccL[i] = 0.0;
+      for (int i = 0; i < NLS; ++i) es.iaccL[i] = 0.f;
       // this wave's Lloyd step words, wave-uniform for the whole sweep
       const int nl = __builtin_amdgcn_readfirstlane(S.nlw[wave]);
       unsigned lw[NLS];
@@ -883,7 +892,8 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       for (int i = 0; i < NLS; ++i)
         lw[i] = __builtin_amdgcn_readfirstlane(i < nl ? S.iw0[S.lstep[wave][i]] : 0u);
 #pragma unroll
-      for (int i = 0; i < NSS; ++i) es.iaccS[i] = 0.0;
+      for (int i = 0; i < NSS; ++i) es.iaccS[i] = 0.f;
+      if (tid < IMAX) S.iinert[tid] = 0.0;  // visible to the flushes after the prologue barrier
       h8 ah[DP / 16], al[DP / 16];
       const bool tact = 32 * ct < ncols;  // wave-uniform
       {
@@ -1022,6 +1032,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
             }
           }
         }
+        if ((t % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
         KM_STAMP(s4);
         // tile t+1 and the E-step operands have landed (this iteration's stores may still be
         // in flight: one per Lloyd step, two per seeding step, issued after every load)
@@ -1045,7 +1056,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       if (blockIdx.x == 0 && lane == 0 && a.stats)
         for (int k = 0; k < 7; ++k) atomicAdd(&a.stats[8 + 8 * wave + k], st_acc[k]);
 #endif
-      estep_finish(S, tid, es);
+      estep_flush(S, tid, es);
       // sums -> Sm (aliases the ring and D: every reader passed the last barrier); counts
       if (mact) {
 #pragma unroll
