@@ -53,6 +53,7 @@ constexpr int SIDE = 8 * KC * FRAG;   // 8 row blocks x 4 chunks = 32 KiB
 constexpr int BUF = 2 * SIDE;         // A side + B side
 constexpr int LDS_BYTES = 2 * BUF;    // double buffered = 128 KiB
 constexpr int NBINS = CC_NBINS;
+constexpr int NW = NT / 64;
 
 __device__ __forceinline__ void tile_coords(int64_t t, int nb, int& bi, int& bj) {
   auto start = [nb](int64_t b) -> int64_t { return b * nb - b * (b - 1) / 2; };
@@ -305,16 +306,30 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
   const int col0 = bj * T + wc * 64 + (lane & 31);
 
   if constexpr (KP == 1) {
-    uint16_t* it = I_tiles_out + tl * (T * T);
+    // thread-contiguous tile layout: thread tid's 128 accumulator elements, in (mi, nj, v)
+    // order, are elements 128 tid .. 128 tid + 127 (16 x 16-B stores; the co-association
+    // epilogue reads them back with 16-B loads)
+    uint4* it4 = reinterpret_cast<uint4*>(I_tiles_out + tl * (T * T) + 128 * tid);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t pk[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            pk[q] = (static_cast<uint32_t>(acc[mi][nj][8 * h + 2 * q]) & 0xFFFFu) |
+                    (static_cast<uint32_t>(acc[mi][nj][8 * h + 2 * q + 1]) << 16);
+          it4[(mi * 2 + nj) * 2 + h] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int nj = 0; nj < 2; ++nj)
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
-          const int e = ((wave * 8 + mi * 2 + nj) * 16 + v) * 64 + lane;
           const int val = acc[mi][nj][v];
-          it[e] = static_cast<uint16_t>(val);
           if (full_out) {
             const int i = row0 + mi * 32 + (v & 3) + 8 * (v >> 2);
             const int j = col0 + nj * 32;
@@ -332,15 +347,16 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     for (int b = 0; b < NBINS; ++b) hist[b * NT + tid] = 0;
     if (tid <= NBINS) es[tid] = edges[tid];
     __syncthreads();
-    const uint16_t* it = I_tiles_in + tl * (T * T);
+    const uint4* it4 = reinterpret_cast<const uint4*>(I_tiles_in + tl * (T * T) + 128 * tid);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int nj = 0; nj < 2; ++nj)
+      for (int nj = 0; nj < 2; ++nj) {
+        const uint4 q0 = it4[(mi * 2 + nj) * 2], q1 = it4[(mi * 2 + nj) * 2 + 1];
+        const uint32_t iw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
-          const int e = ((wave * 8 + mi * 2 + nj) * 16 + v) * 64 + lane;
-          const uint32_t ival = it[e];
+          const uint32_t ival = (iw[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
           const int val = acc[mi][nj][v];
           const int i = row0 + mi * 32 + (v & 3) + 8 * (v >> 2);
           const int j = col0 + nj * 32;
@@ -353,10 +369,23 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
             if (!diag) full_out[static_cast<int64_t>(j) * n + i] = val;
           }
         }
+      }
+    // per-bin totals: every thread reads its own counters, a wave sums its 64 lanes into
+    // LDS, and 20 threads add the 8 wave sums: one global atomic per bin and tile (20
+    // contended words: keep it at one per bin)
+    uint32_t* wsum = reinterpret_cast<uint32_t*>(lds + NBINS * NT * sizeof(uint32_t) + 32 * sizeof(float));
+#pragma unroll
+    for (int b = 0; b < NBINS; ++b) {
+      uint32_t c = hist[b * NT + tid];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+      if (lane == 0) wsum[b * NW + wave] = c;
+    }
     __syncthreads();
     if (tid < NBINS) {
       uint32_t sum = 0;
-      for (int k = 0; k < NT; ++k) sum += hist[tid * NT + k];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sum += wsum[tid * NW + w];
       if (sum) atomicAdd(&bin_counts[tid], static_cast<unsigned long long>(sum));
     }
   }
