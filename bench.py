@@ -40,7 +40,8 @@ CONFIGS = {
     "c2": dict(n=10_000, d=64, k_true=6, Ks=list(range(2, 16)), H=500, frac=0.8),
     "c5": dict(n=200_000, d=32, k_true=6, Ks=list(range(2, 11)), H=256, frac=0.8),
     # BASELINE.json configs[3]: wide rows (cc_kmeans_wide)
-    "c4": dict(n=5_000, d=20_000, k_true=6, Ks=list(range(2, 13)), H=1000, frac=0.8),
+    "c4": dict(n=5_000, d=20_000, k_true=5, Ks=list(range(2, 13)), H=1000, frac=0.8,
+               data="expression"),
     "smoke": dict(n=4_000, d=32, k_true=5, Ks=list(range(2, 8)), H=64, frac=0.8),
 }
 # MI355X_MICROARCH.md: f16/bf16 dense MFMA peak 256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz.  One
@@ -59,6 +60,19 @@ def make_blobs_f32(n, d, k, seed=0):
     X, _ = make_blobs(n_samples=n, n_features=d, centers=k, cluster_std=1.0,
                       center_box=(-10.0, 10.0), shuffle=True, random_state=seed)
     return X.astype(np.float32)
+
+
+def make_expression_f32(n, d, groups=5, informative=500, shift_std=2.0, seed=0):
+    """BASELINE config 4's gene-expression-like rows: n samples in `groups`
+    groups; the first `informative` features carry a per-group mean shift ~ N(0, shift_std^2),
+    every feature has N(0, 1) noise; float32."""
+    rs = np.random.RandomState(seed)
+    g = rs.randint(0, groups, size=n)
+    means = np.zeros((groups, d), dtype=np.float32)
+    means[:, :informative] = rs.normal(0.0, shift_std, size=(groups, informative))
+    X = rs.standard_normal((n, d)).astype(np.float32)
+    X += means[g]
+    return X
 
 
 def cpu_baseline(cfg, X, budget_s=25.0):
@@ -144,7 +158,12 @@ def main():
 
     from consensus_clustering_amd import ConsensusClustering, engine
 
-    X = make_blobs_f32(cfg["n"], cfg["d"], cfg["k_true"], seed=SEED)
+    if cfg.get("data") == "expression":
+        X = make_expression_f32(cfg["n"], cfg["d"], groups=cfg["k_true"], seed=SEED)
+        data = "synthetic gene-expression-like (5 groups, 500 informative features, N(0,1) noise, float32, seed 0)"
+    else:
+        X = make_blobs_f32(cfg["n"], cfg["d"], cfg["k_true"], seed=SEED)
+        data = "synthetic (make_blobs, float32, seed 0)"
     Xd = torch.from_numpy(X).to(dev)  # inputs resident in HBM before the timed region
     cc = ConsensusClustering(K_range=cfg["Ks"], n_iterations=cfg["H"], subsampling=cfg["frac"],
                              random_state=SEED, plot_cdf=False, keep_matrices=False)
@@ -206,8 +225,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f16x3 hi/lo, f32 accumulate (k-means MFMA) / i8 (co-association MFMA)",
-            "data": "synthetic (make_blobs, float32, seed 0)",
-            "config": {"workload": (f"{args.config}: blobs n={cfg['n']} d={d} k_true={cfg['k_true']}, "
+            "data": data,
+            "config": {"workload": (f"{args.config}: {cfg.get('data', 'blobs')} n={cfg['n']} d={d} k_true={cfg['k_true']}, "
                                     f"K={cfg['Ks'][0]}..{cfg['Ks'][-1]}, H={cfg['H']}, "
                                     f"subsampling={cfg['frac']}, n_init=3, full consensus fit"),
                        "n": cfg["n"], "d": d, "K_range": [cfg["Ks"][0], cfg["Ks"][-1]],

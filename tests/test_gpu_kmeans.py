@@ -149,3 +149,25 @@ def test_wide_c4_shape():
                 ref = O.kmeans_labels(X[idx[h]], K, seed, n_init=3)
                 assert np.array_equal(ref, labs[k, h]), (K, h, np.mean(ref == labs[k, h]))
     assert np.all(np.isfinite(inert))
+
+
+def test_wide_expression_like():
+    """BASELINE config 4's data family (bench.make_expression_f32: 5 groups, 500 informative
+    features in N(0,1) noise) at a reduced size: labels agree with sklearn's on most problems
+    (near-ties in noisy data may flip, as between sklearn's own f32 and f64 runs)."""
+    from threadpoolctl import threadpool_limits
+
+    from bench import make_expression_f32
+
+    X = make_expression_f32(1000, 3000, seed=3)
+    Ks, H, seed = [2, 3, 5, 7], 3, 0
+    idx, labs, inert, nit, stats = run_gpu(X, Ks, H, 0.8, seed)
+    agree = total = 0
+    with threadpool_limits(8):
+        for k, K in enumerate(Ks):
+            for h in range(H):
+                ref = O.kmeans_labels(X[idx[h]], K, seed, n_init=3)
+                agree += np.array_equal(ref, labs[k, h])
+                total += 1
+    assert agree >= 0.7 * total, f"{agree}/{total}"
+    assert np.all(np.isfinite(inert))
