@@ -240,12 +240,53 @@ class ConsensusClustering:
         self.best_k_ = post.best_k(self.pac_area_)
 
     # ------------------------------------------------------------------ extras
+    def _device_counts(self, K):
+        """int32 M and I (n x n, on the GPU) of one K, recomputed from the fitted label
+        matrix (CC.py:264 and :287-290) when the fit did not keep them."""
+        if getattr(self, 'labels_', None) is None:
+            raise ValueError("fit() first")
+        Ks = list(self.cdf_at_K_data)
+        k = Ks.index(K)
+        n = self._N
+        labels = self.labels_
+        Hpad = labels.shape[2]
+        nt = engine.num_tiles(n)
+        I_tiles, I_full = engine.cosample(labels[0], n, Hpad, 0, nt, want_full=True)
+        counts = torch.zeros(post.N_BINS, dtype=torch.int64, device=labels.device)
+        M = torch.zeros((n, n), dtype=torch.int32, device=labels.device)
+        engine.coassoc(labels[k], n, Hpad, K, 0, nt, I_tiles, engine.edges_device(labels.device),
+                       counts, M)
+        return M, I_full
+
     def consensus_matrix(self, K):
-        """float32 C for one K (computed on demand on the GPU when not kept)."""
+        """float32 C for one K (CC.py:372-373), recomputed on the GPU when not kept."""
         v = self.cdf_at_K_data[K]
         if v.get('cij') is not None:
             return v['cij']
-        raise ValueError("consensus matrices were not kept (keep_matrices=False)")
+        M, I = self._device_counts(K)
+        return engine.consensus(M, I).cpu().numpy()
+
+    def export_memmap(self, folder=None, Ks=None):
+        """Write each K's co-association counts as the reference's process-mode file
+        (CC.py:147-159): ``<folder>/_temp_{K}``, a raw C-order n x n array of the count dtype
+        (uint8 if n_iterations < 256 else uint16), readable with
+        ``np.memmap(path, dtype, mode='r', shape=(n, n))``.  Returns {K: path}."""
+        import os
+
+        folder = self.memmap_folder if folder is None else folder
+        os.makedirs(folder, exist_ok=True)
+        out = {}
+        for K in (self.cdf_at_K_data if Ks is None else Ks):
+            mij = self.cdf_at_K_data[K].get('mij')
+            if mij is None:
+                mij = self._device_counts(K)[0].cpu().numpy().astype(self._dtype)
+            path = os.path.join(folder, f'_temp_{K}')
+            mm = np.memmap(path, dtype=self._dtype, shape=(self._N, self._N), mode='w+')
+            mm[:] = mij
+            mm.flush()
+            del mm
+            out[K] = path
+        return out
 
     def predict(self, K=None):
         """Consensus labels: average-linkage agglomerative clustering of 1 - C for K
