@@ -54,6 +54,10 @@ constexpr int BUF = 2 * SIDE;         // A side + B side
 constexpr int LDS_BYTES = 2 * BUF;    // double buffered = 128 KiB
 constexpr int NBINS = CC_NBINS;
 constexpr int NW = NT / 64;
+// epilogue LDS: hist [NBINS][NT] u32 | 32 edges f32 | wave sums [NBINS][NW] u32 | bin table
+constexpr int BT_OFF = NBINS * NT * 4 + 32 * 4 + NBINS * NW * 4;
+constexpr int BT_MAX_ROWS = (LDS_BYTES - BT_OFF - 16) / ((NBINS + 1) * 2);
+static_assert(BT_OFF % 16 == 0, "table copies are 16-B");
 
 __device__ __forceinline__ void tile_coords(int64_t t, int nb, int& bi, int& bj) {
   auto start = [nb](int64_t b) -> int64_t { return b * nb - b * (b - 1) / 2; };
@@ -76,6 +80,43 @@ __device__ __forceinline__ int consensus_bin(uint32_t m, uint32_t i, const float
   if (x < e[b]) b -= 1;
   if (b != NBINS - 1 && x >= e[b + 1]) b += 1;
   return b;
+}
+
+// The same bin from the per-co-sampling-count threshold table (cc_bin_table): row i holds
+// T[b] = min{m : consensus_bin(m, i) >= b} for b = 0..20 (T[0] = 0, T[20] = 0xFFFF), so the bin
+// is #{b in 1..19 : m >= T[b]}.  A reciprocal estimate of 20 m / i is within one bin of it and
+// one compare on each side makes it exact: no division, no f64.
+constexpr int BT_ROW = NBINS + 1;
+
+__device__ __forceinline__ int table_bin(uint32_t m, uint32_t i, const uint16_t* tab) {
+  int g = 0;
+  if (i > 0) {
+    g = static_cast<int>(static_cast<float>(m) * (20.0f * __builtin_amdgcn_rcpf(static_cast<float>(i))));
+    g = g > NBINS - 1 ? NBINS - 1 : g;
+  }
+  const uint16_t* row = tab + i * BT_ROW;
+  return g - (m < row[g] ? 1 : 0) + (m >= row[g + 1] ? 1 : 0);
+}
+
+__global__ void bin_table_kernel(int rows, const float* __restrict__ edges, uint16_t* __restrict__ table) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= rows * BT_ROW) return;
+  const int i = e / BT_ROW, b = e - i * BT_ROW;
+  uint32_t t;
+  if (b == 0) {
+    t = 0;
+  } else if (b == NBINS) {
+    t = 0xFFFFu;
+  } else {  // first m in [0, i] with bin >= b (monotone in m), i + 1 if none
+    uint32_t lo = 0, hi = static_cast<uint32_t>(i) + 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (consensus_bin(mid, static_cast<uint32_t>(i), edges) >= b) hi = mid;
+      else lo = mid + 1;
+    }
+    t = lo;
+  }
+  table[e] = static_cast<uint16_t>(t);
 }
 
 // Load the HS = 128/KP label bytes of one row for one super-step into w[].
@@ -174,7 +215,7 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     const uint8_t* __restrict__ labels, int n, int ldl, int Hpad, int64_t tile_begin,
     uint16_t* __restrict__ I_tiles_out, const uint16_t* __restrict__ I_tiles_in,
     const float* __restrict__ edges, unsigned long long* __restrict__ bin_counts,
-    int32_t* __restrict__ full_out) {
+    int32_t* __restrict__ full_out, const uint16_t* __restrict__ btab, int bt_rows) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   constexpr int HS = 128 / KP;  // resamples per super-step
 
@@ -340,12 +381,20 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           }
         }
   } else {
-    // [NBINS][NT] private counters + the 21 edges, reusing the operand LDS.
+    // [NBINS][NT] private counters, the 21 edges, the per-wave sums and (small H) the bin
+    // threshold table, reusing the operand LDS.
     uint32_t* hist = reinterpret_cast<uint32_t*>(lds);
     float* es = reinterpret_cast<float*>(lds + NBINS * NT * sizeof(uint32_t));
+    uint16_t* tab = reinterpret_cast<uint16_t*>(lds + BT_OFF);
 #pragma unroll
     for (int b = 0; b < NBINS; ++b) hist[b * NT + tid] = 0;
     if (tid <= NBINS) es[tid] = edges[tid];
+    if (btab) {  // 16-B copies (the table allocation is padded to 16 B)
+      const int vecs = (bt_rows * BT_ROW * 2 + 15) / 16;
+      const uint4* src = reinterpret_cast<const uint4*>(btab);
+      uint4* dst = reinterpret_cast<uint4*>(tab);
+      for (int e = tid; e < vecs; e += NT) dst[e] = src[e];
+    }
     __syncthreads();
     const uint4* it4 = reinterpret_cast<const uint4*>(I_tiles_in + tl * (T * T) + 128 * tid);
 #pragma unroll
@@ -361,7 +410,8 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           const int i = row0 + mi * 32 + (v & 3) + 8 * (v >> 2);
           const int j = col0 + nj * 32;
           if (i < j && j < n) {
-            const int b = consensus_bin(static_cast<uint32_t>(val), ival, es);
+            const int b = btab ? table_bin(static_cast<uint32_t>(val), ival, tab)
+                               : consensus_bin(static_cast<uint32_t>(val), ival, es);
             atomicAdd(&hist[b * NT + tid], 1u);
           }
           if (full_out && i < n && j < n) {
@@ -444,9 +494,10 @@ int launch_status(const char* fn) {
 template <int KP>
 void launch_tiles(dim3 grid, hipStream_t st, const uint8_t* lab, int n, int ldl, int Hpad,
                   int64_t tb, uint16_t* Iout, const uint16_t* Iin, const float* edges,
-                  unsigned long long* counts, int32_t* full) {
+                  unsigned long long* counts, int32_t* full, const uint16_t* btab = nullptr,
+                  int bt_rows = 0) {
   hipLaunchKernelGGL(tiles_kernel<KP>, grid, dim3(NT), 0, st, lab, n, ldl, Hpad, tb, Iout, Iin,
-                     edges, counts, full);
+                     edges, counts, full, btab, bt_rows);
 }
 
 }  // namespace
@@ -492,10 +543,24 @@ extern "C" int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, in
   return launch_status("cc_cosample");
 }
 
+// table: rows * 21 uint16, allocated to a multiple of 16 B (cc_coassoc copies it in 16-B pieces)
+extern "C" int cc_bin_table(int rows, const float* edges, uint16_t* table, void* stream) {
+  if (rows <= 0 || rows > BT_MAX_ROWS || !edges || !table) {
+    cc::set_error("cc_bin_table: bad arguments (1 <= rows <= cc_bin_table_max_rows())");
+    return CC_ERR_ARG;
+  }
+  const int total = rows * BT_ROW;
+  hipLaunchKernelGGL(bin_table_kernel, dim3((total + 255) / 256), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), rows, edges, table);
+  return launch_status("cc_bin_table");
+}
+
+extern "C" int cc_bin_table_max_rows(void) { return BT_MAX_ROWS; }
+
 extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int K,
                           int64_t tile_begin, int64_t tile_end, const uint16_t* I_tiles,
                           const float* edges, unsigned long long* bin_counts, int32_t* M_full,
-                          void* stream) {
+                          const uint16_t* bin_table, int table_rows, void* stream) {
   int rc = check_common("cc_coassoc", labels_nh, n, ldl, Hpad, tile_begin, tile_end);
   if (rc) return rc;
   if (K < 1 || K > 127) {
@@ -504,6 +569,10 @@ extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int
   }
   if (!I_tiles || !edges || !bin_counts) {
     cc::set_error("cc_coassoc: I_tiles, edges and bin_counts are required");
+    return CC_ERR_ARG;
+  }
+  if (bin_table && (table_rows < Hpad + 1 || table_rows > BT_MAX_ROWS)) {
+    cc::set_error("cc_coassoc: bin_table needs Hpad + 1 <= table_rows <= cc_bin_table_max_rows()");
     return CC_ERR_ARG;
   }
   const int64_t ntl = tile_end - tile_begin;
@@ -518,13 +587,13 @@ extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int
   int kp = 2;
   while (kp < K) kp <<= 1;
   switch (kp) {
-    case 2: launch_tiles<2>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
-    case 4: launch_tiles<4>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
-    case 8: launch_tiles<8>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
-    case 16: launch_tiles<16>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
-    case 32: launch_tiles<32>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
-    case 64: launch_tiles<64>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
-    default: launch_tiles<128>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full); break;
+    case 2: launch_tiles<2>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    case 4: launch_tiles<4>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    case 8: launch_tiles<8>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    case 16: launch_tiles<16>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    case 32: launch_tiles<32>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    case 64: launch_tiles<64>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    default: launch_tiles<128>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
   }
   return launch_status("cc_coassoc");
 }

@@ -135,15 +135,36 @@ def edges_device(device) -> torch.Tensor:
     return torch.from_numpy(bin_edges32().copy()).to(device)
 
 
+_BIN_TABLES = {}
+
+
+def bin_table(device, rows: int):
+    """Cached cc_bin_table thresholds for co-sampling counts [0, rows), or None when the table
+    is too large to stage on chip (cc_coassoc then bins by division)."""
+    if rows > _lib.load().cc_bin_table_max_rows():
+        return None
+    key = (str(device), rows)
+    t = _BIN_TABLES.get(key)
+    if t is None:
+        words = (rows * (N_BINS + 1) + 7) // 8 * 8  # 16-B padded allocation
+        t = torch.zeros(words, dtype=torch.int16, device=device)
+        _lib.call("cc_bin_table", rows, edges_device(device).data_ptr(), t.data_ptr(),
+                  stream_ptr())
+        _BIN_TABLES[key] = t
+    return t
+
+
 def coassoc(labels_nh: torch.Tensor, n: int, Hpad: int, K: int, tile_begin: int, tile_end: int,
             I_tiles: torch.Tensor, edges: torch.Tensor, counts: torch.Tensor,
-            M_full: torch.Tensor = None):
+            M_full: torch.Tensor = None, use_table: bool = True):
     """Accumulate the strict-upper-pair histogram of C for one K into counts (int64[20])."""
     assert counts.dtype == torch.int64 and counts.numel() == N_BINS
+    tab = bin_table(labels_nh.device, Hpad + 1) if use_table else None
     with timed("cc_coassoc"):
         _lib.call("cc_coassoc", labels_nh.data_ptr(), n, labels_nh.stride(0), Hpad, int(K),
                   tile_begin, tile_end, I_tiles.data_ptr(), edges.data_ptr(), counts.data_ptr(),
-                  _lib.ptr(M_full), stream_ptr())
+                  _lib.ptr(M_full), _lib.ptr(tab), Hpad + 1 if tab is not None else 0,
+                  stream_ptr())
 
 
 def consensus(M: torch.Tensor, I: torch.Tensor) -> torch.Tensor:

@@ -81,10 +81,21 @@ int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, int64_t tile_
  * over the strict upper triangle i < j (CC.py:287-290, :338-344).
  * edges: 21 float32 bin edges (numpy's), device.  bin_counts: [20] uint64, device,
  * accumulated into (not cleared).  M_full: optional [n][n] int32, may be NULL.
- * K <= 127. */
+ * bin_table: optional cc_bin_table output with table_rows >= Hpad + 1 rows (binning without
+ * a division; identical bins), NULL for the division path.  K <= 127. */
 int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int K, int64_t tile_begin,
                int64_t tile_end, const uint16_t* I_tiles, const float* edges,
-               unsigned long long* bin_counts, int32_t* M_full, void* stream);
+               unsigned long long* bin_counts, int32_t* M_full, const uint16_t* bin_table,
+               int table_rows, void* stream);
+
+/* Bin thresholds per co-sampling count i in [0, rows): row i = 21 uint16 T[b] =
+ * min{m : bin(f32(m) / f32(i + 1e-6)) >= b} (T[0] = 0, T[20] = 0xFFFF; i + 1 if no m <= i
+ * reaches b), so bin = #{b in 1..19 : m >= T[b]} (numpy.histogram semantics, CC.py:338-344).
+ * table: device, rows * 21 uint16 in an allocation padded to a multiple of 16 B. */
+int cc_bin_table(int rows, const float* edges, uint16_t* table, void* stream);
+
+/* Largest table (rows) cc_coassoc can stage on chip. */
+int cc_bin_table_max_rows(void);
 
 /* C = f32(M) / f32(f64(I) + 1e-6) with C_ii = 1 (CC.py:372-373), [n][n]. */
 int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stream);

@@ -124,3 +124,33 @@ def test_consensus_matrix_kernel():
     M = (I * rng.random((n, n))).astype(np.int32)
     C = engine.consensus(torch.from_numpy(M).to(dev), torch.from_numpy(I).to(dev)).cpu().numpy()
     np.testing.assert_array_equal(C, O.consensus_matrix(M.astype(np.uint16), I.astype(np.uint16)))
+
+
+@pytest.mark.parametrize("H,K", [(37, 3), (300, 7), (1000, 20)])
+def test_threshold_table_binning_is_exact(H, K):
+    """cc_coassoc's division-free binning (cc_bin_table thresholds) gives the same 20 counts as
+    the direct numpy-exact bin on every pair; the table itself matches the host oracle's
+    per-pair bin for every (m <= i) it covers."""
+    dev = engine.require_gpu()
+    n = 700
+    rs = np.random.RandomState(H)
+    idx = np.stack([rs.permutation(n)[: int(0.8 * n)] for _ in range(H)])
+    labs = [rs.randint(0, K, size=idx.shape)]
+    L, Hpad = _device_labels(idx, labs, n, H, dev)
+    nt = engine.num_tiles(n)
+    edges = engine.edges_device(dev)
+    I_tiles, _ = engine.cosample(L[0], n, Hpad, 0, nt, want_full=False)
+    c_tab = torch.zeros(20, dtype=torch.int64, device=dev)
+    c_div = torch.zeros(20, dtype=torch.int64, device=dev)
+    engine.coassoc(L[0], n, Hpad, K, 0, nt, I_tiles, edges, c_tab, use_table=True)
+    engine.coassoc(L[0], n, Hpad, K, 0, nt, I_tiles, edges, c_div, use_table=False)
+    np.testing.assert_array_equal(c_tab.cpu().numpy(), c_div.cpu().numpy())
+    assert int(c_tab.sum()) == n * (n - 1) // 2
+    tab = engine.bin_table(dev, Hpad + 1).cpu().numpy().view(np.uint16)[: (H + 1) * 21].reshape(H + 1, 21)
+    e32 = np.linspace(0, 1, 21, dtype=np.float32)
+    for i in range(0, H + 1, max(1, H // 40)):
+        m = np.arange(i + 1)
+        x = np.float32(m) / np.float32(np.float64(i) + 1e-6)
+        ref = np.clip(np.searchsorted(e32, x, side="right") - 1, 0, 19)
+        got = (m[:, None] >= tab[i, 1:20][None, :]).sum(axis=1)
+        np.testing.assert_array_equal(got, ref, err_msg=f"i={i}")
