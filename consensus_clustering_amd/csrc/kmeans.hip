@@ -1015,20 +1015,29 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
             mcnt += nb;
             const h8 oh = __builtin_bit_cast(h8, ohu);
             const int row0 = 16 * s2 + 8 * (G >> 1) + q;
-#pragma unroll
-            for (int dt = 0; dt < DP / 32; ++dt) {
+            // transposed B reads one feature block ahead of its MFMAs (the LDS latency of
+            // block dt+1 hides under block dt's two MFMAs)
+            auto rd = [&](int dt, s4 (&r)[4]) __attribute__((always_inline)) {
               const int chn = 4 * dt + 2 * (G & 1) + (pp >> 1);
               const int a0 = xoff<DP>(row0, chn) + 8 * (pp & 1);
               const int a1 = xoff<DP>(row0 + 4, chn) + 8 * (pp & 1);
-              const s4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a0));
-              const s4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a1));
-              const s4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a0));
-              const s4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a1));
-              const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
-              const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7));
+              r[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a0));
+              r[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a1));
+              r[2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a0));
+              r[3] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a1));
+            };
+            s4 rc[4], rn[4];
+            rd(0, rc);
+#pragma unroll
+            for (int dt = 0; dt < DP / 32; ++dt) {
+              if (dt + 1 < DP / 32) rd(dt + 1, rn);
+              const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(rc[0], rc[1], 0, 1, 2, 3, 4, 5, 6, 7));
+              const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(rc[2], rc[3], 0, 1, 2, 3, 4, 5, 6, 7));
               sacc[dt] = mfma16(oh, bl, sacc[dt]);
               sacc[dt] = mfma16(oh, bh, sacc[dt]);
               __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+              for (int k = 0; k < 4; ++k) rc[k] = rn[k];
             }
           }
         }
