@@ -240,6 +240,7 @@ def main():
                 "frac": achieved / KMEANS_PEAK_TF,
                 "peak_note": "f16 dense MFMA peak 2516.6 TF / 3 (f32-class product = 3 f16 MFMAs)",
                 "sweeps": float(st[4]), "slot_tile_row_tiles": float(st[5]),
+                "relocations": float(st[3]),
                 "traffic": traffic,
                 "flops_per_launch": flops / km_launches,
                 "avg_launch_ms": km_ms_tot / km_launches,

@@ -715,20 +715,59 @@ __device__ void kpp_select(const WArgs& a, WProb& q, const float* closest, int l
   }
 }
 
-// squared norm of a centre row (f64 sum, one wave) -> f32, and its f16 hi/lo image
-__device__ void finish_row(const WArgs& a, const float* c, uint16_t* hl, float* norm, int lane) {
-  double s = 0.0;
-  for (int d = lane; d < a.dpad; d += 64) {
-    const float x = c[d];
-    if (d < a.dreal) s += static_cast<double>(x) * static_cast<double>(x);
-    const float xs = x * a.scale;
-    const _Float16 hi = static_cast<_Float16>(xs);
-    const _Float16 lo = static_cast<_Float16>(xs - static_cast<float>(hi));
-    hl[d] = __builtin_bit_cast(uint16_t, hi);
-    hl[a.dpad + d] = __builtin_bit_cast(uint16_t, lo);
+
+// One new centre row (one wave): nw <- nw * alpha (the f32 _average_centers scaling, in
+// place), shift = |nw - od|^2 (f64 sum -> f32, squared back from its f32 root as
+// _euclidean_dense_dense + `** 2`), the f16 hi/lo image and the f32 squared norm.  Four 16-B
+// pieces per lane in flight.
+__device__ void update_row(const WArgs& a, float* nw, const float* od, float alpha, uint16_t* hl,
+                           float* norm, float* shift, int lane) {
+  const int n4 = a.dpad / 4;
+  double sh = 0.0, nn = 0.0;
+  for (int q0 = lane; q0 < n4; q0 += 256) {
+    float4 x[4], o[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int qi = q0 + 64 * u;
+      if (qi < n4) {
+        x[u] = reinterpret_cast<const float4*>(nw)[qi];
+        o[u] = reinterpret_cast<const float4*>(od)[qi];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int qi = q0 + 64 * u;
+      if (qi >= n4) continue;
+      const float v[4] = {x[u].x * alpha, x[u].y * alpha, x[u].z * alpha, x[u].w * alpha};
+      const float w[4] = {o[u].x, o[u].y, o[u].z, o[u].w};
+      reinterpret_cast<float4*>(nw)[qi] = make_float4(v[0], v[1], v[2], v[3]);
+      uint16_t h[4], l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (4 * qi + k < a.dreal) {
+          const double t = static_cast<double>(v[k]) - static_cast<double>(w[k]);
+          sh += t * t;
+          nn += static_cast<double>(v[k]) * static_cast<double>(v[k]);
+        }
+        const float xs = v[k] * a.scale;
+        const _Float16 hi = static_cast<_Float16>(xs);
+        const _Float16 lo = static_cast<_Float16>(xs - static_cast<float>(hi));
+        h[k] = __builtin_bit_cast(uint16_t, hi);
+        l[k] = __builtin_bit_cast(uint16_t, lo);
+      }
+      reinterpret_cast<uint2*>(hl)[qi] = make_uint2(h[0] | (static_cast<uint32_t>(h[1]) << 16),
+                                                    h[2] | (static_cast<uint32_t>(h[3]) << 16));
+      reinterpret_cast<uint2*>(hl + a.dpad)[qi] = make_uint2(l[0] | (static_cast<uint32_t>(l[1]) << 16),
+                                                             l[2] | (static_cast<uint32_t>(l[3]) << 16));
+    }
   }
-  s = wave_sum(s);
-  if (lane == 0) *norm = static_cast<float>(s);
+  sh = wave_sum(sh);
+  nn = wave_sum(nn);
+  if (lane == 0) {
+    const float r = sqrtf(static_cast<float>(sh));
+    *shift = r * r;
+    *norm = static_cast<float>(nn);
+  }
 }
 
 // Empty-cluster relocation for problem p (rare; _k_means_common.pyx:167-212).  sums: the
@@ -737,19 +776,25 @@ __device__ void relocate(const WArgs& a, PS& L, const int32_t* idx, int p, float
                          const uint8_t* lab, float* dist, int tid) {
   WProb& q = L.S.pr[p];
   const int m = a.m, K = q.K, dpad = a.dpad, off = q.cenoff;
+  // squared distance of every row to the centre it was assigned to: one wave per row,
+  // coalesced 16-B reads, f64 sum of the f32 squared differences
+  const int lane = tid & 63, wave = tid >> 6, n4 = dpad / 4;
   float mymax = 0.f;
-  for (int r = tid; r < m; r += NT) {
-    const float* x = a.X + static_cast<size_t>(idx[r]) * dpad;
-    const float* c = cold + static_cast<size_t>(lab[r]) * dpad;
-    float s = 0.f;
-    for (int d = 0; d < a.dreal; ++d) {
-      const float t = x[d] - c[d];
-      s = fmaf(t, t, s);
+  for (int r = wave; r < m; r += NW) {
+    const float4* x = reinterpret_cast<const float4*>(a.X + static_cast<size_t>(idx[r]) * dpad);
+    const float4* c = reinterpret_cast<const float4*>(cold + static_cast<size_t>(lab[r]) * dpad);
+    double acc = 0.0;
+    for (int q = lane; q < n4; q += 64) {
+      const float4 xv = x[q], cv = c[q];
+      const float t[4] = {xv.x - cv.x, xv.y - cv.y, xv.z - cv.z, xv.w - cv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * q + k < a.dreal) acc += static_cast<double>(t[k]) * static_cast<double>(t[k]);
     }
-    dist[r] = s;
-    mymax = fmaxf(mymax, s);
+    const float sd = static_cast<float>(wave_sum(acc));
+    if (lane == 0) dist[r] = sd;
+    mymax = fmaxf(mymax, sd);
   }
-  for (int o = 32; o > 0; o >>= 1) mymax = fmaxf(mymax, __shfl_xor(mymax, o));
   if ((tid & 63) == 0) L.red_v[tid >> 6] = mymax;
   __syncthreads();
   double gmax = 0.0;
@@ -995,17 +1040,8 @@ __device__ void post_body(const WArgs& a, PS& L, bool init) {
         kpp_select(a, q, R.dbuf + (static_cast<size_t>(p) * a.ndb + q.cs) * a.lsm, lane);
       }
     }
-    // initial centres of problems leaving seeding: the chosen rows (exact f32)
-    for (int p = 0; p < P; ++p) {
-      const WProb& q = S.pr[p];
-      if (!q.to_run) continue;
-      for (int c = 0; c < q.K; ++c) {
-        const float4* src = reinterpret_cast<const float4*>(a.X + static_cast<size_t>(idx[R.cpos[p * a.kws + c]]) * dpad);
-        float4* dst = reinterpret_cast<float4*>(R.cen + (static_cast<size_t>(q.ccur) * Cn + q.cenoff + c) * dpad);
-        for (int d = tid; d < dpad / 4; d += NT) dst[d] = src[d];
-      }
-    }
-    __syncthreads();
+    // initial centres of problems leaving seeding: the chosen rows (exact f32), their f16 image
+    // and norm (one wave per row; a lane reads back only what it wrote)
     {
       int j = 0;
       for (int p = 0; p < P; ++p) {
@@ -1014,8 +1050,11 @@ __device__ void post_body(const WArgs& a, PS& L, bool init) {
         for (int c = 0; c < q.K; ++c) {
           if ((j++ % NW) != wave) continue;
           const int row = q.cenoff + c;
-          finish_row(a, R.cen + (static_cast<size_t>(q.ccur) * Cn + row) * dpad, R.cenhl + static_cast<size_t>(row) * 2 * dpad,
-                     R.cenn + row, lane);
+          const float4* src = reinterpret_cast<const float4*>(a.X + static_cast<size_t>(idx[R.cpos[p * a.kws + c]]) * dpad);
+          float* dst = R.cen + (static_cast<size_t>(q.ccur) * Cn + row) * dpad;
+          for (int d = lane; d < dpad / 4; d += 64) reinterpret_cast<float4*>(dst)[d] = src[d];
+          update_row(a, dst, dst, 1.f, R.cenhl + static_cast<size_t>(row) * 2 * dpad, R.cenn + row,
+                     L.shift + row, lane);
         }
       }
     }
@@ -1089,53 +1128,60 @@ __device__ void post_body(const WArgs& a, PS& L, bool init) {
     }
     __syncthreads();
     // _average_centers (_k_means_common.pyx:215-237) runs j in order: an empty cluster j copies
-    // centre argmax(weight), which is still a raw sum when j < argmax.
-    for (int pass = 0; pass < 3; ++pass) {
-      for (int p = 0; p < P; ++p) {
-        if (!ran(p)) continue;
-        const WProb& q = S.pr[p];
-        if (pass != 1 && q.nempty == 0) continue;
-        float* base = R.cen + (static_cast<size_t>(1 - q.ccur) * Cn + q.cenoff) * dpad;
-        for (int c = 0; c < q.K; ++c) {
-          const unsigned cn = L.cnt[q.cenoff + c];
-          float* row = base + static_cast<size_t>(c) * dpad;
-          if (pass == 1) {
-            if (cn == 0) continue;
-            const float alpha = static_cast<float>(1.0 / static_cast<double>(static_cast<float>(cn)));
-            for (int d = tid; d < dpad; d += NT) row[d] *= alpha;
-          } else {
-            if (cn != 0 || (pass == 0 ? c > q.amax : c < q.amax)) continue;
-            const float* src = base + static_cast<size_t>(q.amax) * dpad;
-            for (int d = tid; d < dpad; d += NT) row[d] = src[d];
-          }
-        }
+    // centre argmax(weight), which is still a raw sum when j < argmax (pass 0 here, rare) and
+    // the averaged one when j > argmax (pass 2 below, rare).  Pass 1, the scaling of every
+    // other row, is fused with the centre shift, the f16 image and the norm: one wave per
+    // row, 16-B accesses, one read of the new and the old row.
+    for (int p = 0; p < P; ++p) {
+      if (!ran(p) || S.pr[p].nempty == 0) continue;
+      const WProb& q = S.pr[p];
+      float* base = R.cen + (static_cast<size_t>(1 - q.ccur) * Cn + q.cenoff) * dpad;
+      for (int c = 0; c < q.amax; ++c) {
+        if (L.cnt[q.cenoff + c] != 0) continue;
+        const float* src = base + static_cast<size_t>(q.amax) * dpad;
+        for (int d = tid; d < dpad; d += NT) base[static_cast<size_t>(c) * dpad + d] = src[d];
       }
-      __syncthreads();
     }
-    // centre shifts |c_new - c_old|^2 (f64 sum, one wave per centre)
-    {
+    __syncthreads();
+    auto finish_rows = [&](bool late) {
       int j = 0;
       for (int p = 0; p < P; ++p) {
         if (!ran(p)) continue;
         const WProb& q = S.pr[p];
         for (int c = 0; c < q.K; ++c) {
+          const unsigned cn = L.cnt[q.cenoff + c];
+          if (late != (cn == 0 && c > q.amax)) continue;  // pass-2 rows are finished after it
           if ((j++ % NW) != wave) continue;
-          const float* cn = R.cen + (static_cast<size_t>(1 - q.ccur) * Cn + q.cenoff + c) * dpad;
-          const float* co = R.cen + (static_cast<size_t>(q.ccur) * Cn + q.cenoff + c) * dpad;
-          double s = 0.0;
-          for (int d = lane; d < a.dreal; d += 64) {
-            const double t = static_cast<double>(cn[d]) - static_cast<double>(co[d]);
-            s += t * t;
-          }
-          s = wave_sum(s);
-          if (lane == 0) {
-            const float sh = sqrtf(static_cast<float>(s));
-            L.shift[q.cenoff + c] = sh * sh;
-          }
+          const int row = q.cenoff + c;
+          const float alpha =
+              (cn > 0 && !late) ? static_cast<float>(1.0 / static_cast<double>(static_cast<float>(cn))) : 1.f;
+          update_row(a, R.cen + (static_cast<size_t>(1 - q.ccur) * Cn + row) * dpad,
+                     R.cen + (static_cast<size_t>(q.ccur) * Cn + row) * dpad, alpha,
+                     R.cenhl + static_cast<size_t>(row) * 2 * dpad, R.cenn + row, L.shift + row, lane);
         }
       }
-    }
+    };
+    finish_rows(false);
     __syncthreads();
+    {
+      bool any = false;
+      for (int p = 0; p < P; ++p) any |= ran(p) && S.pr[p].nempty > 0;
+      if (any) {
+        for (int p = 0; p < P; ++p) {
+          if (!ran(p) || S.pr[p].nempty == 0) continue;
+          const WProb& q = S.pr[p];
+          float* base = R.cen + (static_cast<size_t>(1 - q.ccur) * Cn + q.cenoff) * dpad;
+          for (int c = q.amax + 1; c < q.K; ++c) {
+            if (L.cnt[q.cenoff + c] != 0) continue;
+            const float* src = base + static_cast<size_t>(q.amax) * dpad;
+            for (int d = tid; d < dpad; d += NT) base[static_cast<size_t>(c) * dpad + d] = src[d];
+          }
+        }
+        __syncthreads();
+        finish_rows(true);
+        __syncthreads();
+      }
+    }
     // convergence decisions (_kmeans_single_lloyd :697-736)
     if (tid < P) {
       WProb& q = S.pr[tid];
@@ -1159,22 +1205,6 @@ __device__ void post_body(const WArgs& a, PS& L, bool init) {
       }
     }
     __syncthreads();
-    // f16 image and norms of the new centres of problems that go on
-    {
-      int j = 0;
-      for (int p = 0; p < P; ++p) {
-        const WProb& q = S.pr[p];
-        if (!ran(p) || q.st == ST_DONE) continue;
-        for (int c = 0; c < q.K; ++c) {
-          if ((j++ % NW) != wave) continue;
-          const int row = q.cenoff + c;
-          finish_row(a, R.cen + (static_cast<size_t>(q.ccur) * Cn + row) * dpad, R.cenhl + static_cast<size_t>(row) * 2 * dpad,
-                     R.cenn + row, lane);
-        }
-      }
-    }
-    __syncthreads();
-
     // ---- all problems done: best of n_init per K, output (KMeans.fit :1495-1531) ----------
     bool all_done = true;
     for (int p = 0; p < P; ++p) all_done &= (S.pr[p].st == ST_DONE);
