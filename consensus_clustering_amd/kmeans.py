@@ -145,7 +145,7 @@ class BatchedKMeans:
     """All (h, K, init) k-means problems of a consensus fit, on one device."""
 
     def __init__(self, Ks, n_init=3, max_iter=300, tol=1e-4, random_state=0,
-                 workspace_budget=8 << 30, seedmax=16, wide_budget=96 << 30):
+                 workspace_budget=8 << 30, seedmax=10, wide_budget=96 << 30):
         self.Ks = [int(k) for k in Ks]
         self.n_init = int(n_init)
         self.max_iter = int(max_iter)
@@ -177,7 +177,7 @@ class BatchedKMeans:
         u_h = plan(self.Ks, self.n_init, n_sub)
         self.units = u_h
         nU = u_h.shape[0]
-        seedmax = max(1, min(self.seedmax, 32, int(u_h[:, 0].max())))
+        seedmax = max(1, min(int(os.environ.get("CCMI_SEEDMAX", 0)) or self.seedmax, 32, int(u_h[:, 0].max())))
         u, pos, stride = kpp_tables(self.Ks, self.n_init, self.seed, m, weight_dtype)
         u_d = torch.from_numpy(u).to(dev)
         pos_d = torch.from_numpy(pos).to(dev)
