@@ -282,7 +282,9 @@ __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
   };
 
   const int S = dpad / KC;
-  const int ws = wave & 3, wr = wave >> 2, lr = lane & 31, hh = lane >> 5;
+  // waves w and w+4 share a SIMD: give them different slot groups (ws = w >> 1), so a tile
+  // with few slots (k-means++ rounds) still keeps every SIMD's matrix pipe busy
+  const int ws = wave >> 1, wr = wave & 1, lr = lane & 31, hh = lane >> 5;
   const bool wact = 64 * ws < nslots;  // wave-uniform
   v16f acc[2][2];
 #pragma unroll
@@ -490,7 +492,7 @@ __global__ __launch_bounds__(NT, 1) void wide_mstep(WArgs a) {
     *reinterpret_cast<uint4*>(ldst0 + buf * ((IMW + 1) * MRS)) = Rg.l;
   };
 
-  const int ws = wave & 3, wd = wave >> 2, lr = lane & 31, hh = lane >> 5;
+  const int ws = wave >> 1, wd = wave & 1, lr = lane & 31, hh = lane >> 5;  // as wide_estep
   const int fw = dt * MDW + 128 * wd;
   const int nbd = min(4, max(0, (dpad - fw) / 32));  // feature blocks of this wave (uniform)
   const bool wact = s_gact[ws] && nbd > 0;
