@@ -47,7 +47,6 @@ constexpr int ER = 128;          // rows per E workgroup
 constexpr int CWW = 256;         // slots per column tile
 constexpr int IMW = 128;         // work items per column tile
 constexpr int KC = 32;           // features per E stage
-constexpr int AP = 80;           // LDS pitch (bytes) of one staged 32-feature f16 row: conflict-free b128
 constexpr int DS = CWW + 4;      // distance-tile row stride (floats)
 constexpr int MDW = 256;         // features per M workgroup
 constexpr int MRS = 32;          // rows per M stage
@@ -187,16 +186,37 @@ __device__ __forceinline__ float np_pairwise_sum(const float* a, int n) {
   return res;
 }
 
+// LDS-DMA piece from inline asm (lane i writes 16 B at M0 + 16 i), opaque to the compiler's
+// waitcnt pass; completion is awaited explicitly with dma_wait_n (vmcnt drains in order).  M0
+// is set inside the asm; nothing else in these kernels uses M0.
+__device__ __forceinline__ void dma_piece16(const void* g, const void* lds_dst) {
+  const unsigned la = static_cast<unsigned>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) const char*)lds_dst));
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g));
+}
+
+template <int N>
+__device__ __forceinline__ void dma_wait_n() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  static_assert(N == 0 || N == 6, "six pieces per wave and stage");
+}
+
 // ============================================================================================
 // E: distances of a 128-row tile to a 256-slot column tile, then the E-step.
 // Waves: 4 slot groups (64 slots) x 2 row groups (64 rows); per 32-feature stage each wave does
 // 2 k-steps x (2 x 2 blocks) x 3 MFMAs from register-staged, double-buffered LDS images.
 // ============================================================================================
 __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
-  constexpr int APL = CWW * AP, BPL = ER * AP;  // one plane of A (slots) / B (rows)
-  constexpr int STG = 2 * APL + 2 * BPL;
+  // ring of 3 stages; a stage = A (slots) hi/lo planes + B (rows) hi/lo planes, 64-B rows
+  // (32 features) with the 16-B chunks XOR-swizzled by (row >> 2) & 3: conflict-free b128
+  // fragment reads, and lane-linear 1-KiB pieces (16 rows of a plane) for the LDS-DMA fill
+  constexpr int RB = KC * 2;                    // 64 B per row and plane
+  constexpr int APL = CWW * RB, BPL = ER * RB;   // 16 KiB, 8 KiB
+  constexpr int STG = 2 * APL + 2 * BPL;        // 48 KiB
+  constexpr int NSTG = 3;
   constexpr int DBYTES = ER * DS * 4;
-  constexpr int UN = (2 * STG > DBYTES) ? 2 * STG : DBYTES;
+  constexpr int UN = (NSTG * STG > DBYTES) ? NSTG * STG : DBYTES;
   __shared__ __attribute__((aligned(16))) char sm[UN];
   __shared__ int s_srow[CWW];
   __shared__ __attribute__((aligned(16))) float s_cn[CWW];
@@ -234,116 +254,101 @@ __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
   }
   __syncthreads();
 
-  // loaders: A = slot tid>>1, plane tid&1 (64 B / stage); B = row tid>>2, plane (tid>>1)&1,
-  // 32-B half tid&1
-  const int sa = tid >> 1, pa = tid & 1;
-  // every lane loads (no divergent loads: the compiler then counts vmcnt exactly); dummy and
-  // unused slots read row s_gidx[0]: a dummy's distance is +inf whatever its A operand
-  const uint16_t* asrc;
-  {
-    const int sr = s_srow[sa];
-    if (sr >= 0) asrc = a.Xhl + (static_cast<size_t>(sr) * 2 + pa) * dpad;
-    else if (sr != INT_MIN) asrc = R.cenhl + (static_cast<size_t>(-sr - 1) * 2 + pa) * dpad;
-    else asrc = a.Xhl + (static_cast<size_t>(s_gidx[0]) * 2 + pa) * dpad;
+  // LDS-DMA fill: per stage 48 pieces of 1 KiB (A: 2 planes x 16, B: 2 planes x 8), six per
+  // wave; lane i of a piece writes 16 B at piece base + 16 i, i.e. row i/4, physical chunk
+  // i%4, so it fetches logical chunk (i%4) ^ ((row >> 2) & 3) of its row.  The source rows
+  // are fixed for the workgroup: six 64-bit pointers per lane, advanced by 64 B per stage.
+  // Dummy slots and slots past nslots read a valid X row (their distances are +inf or unread).
+  const int S = dpad / KC;
+  const char* psrc[6];
+  int pdst[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int pc = wave + NW * k;  // piece of the stage
+    int row, plane, base;
+    if (pc < 32) {
+      plane = pc >> 4;
+      row = (pc & 15) * 16 + (lane >> 2);
+      base = plane * APL + (pc & 15) * 1024;
+    } else {
+      plane = (pc - 32) >> 3;
+      row = ((pc - 32) & 7) * 16 + (lane >> 2);
+      base = 2 * APL + plane * BPL + ((pc - 32) & 7) * 1024;
+    }
+    const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+    const uint16_t* src;
+    if (pc < 32) {
+      const int sr = s_srow[row];
+      if (sr >= 0) src = a.Xhl + (static_cast<size_t>(sr) * 2 + plane) * dpad;
+      else if (sr != INT_MIN) src = R.cenhl + (static_cast<size_t>(-sr - 1) * 2 + plane) * dpad;
+      else src = a.Xhl + (static_cast<size_t>(s_gidx[0]) * 2 + plane) * dpad;
+    } else {
+      src = a.Xhl + (static_cast<size_t>(s_gidx[row]) * 2 + plane) * dpad;
+    }
+    psrc[k] = reinterpret_cast<const char*>(src) + 16 * chunk;
+    pdst[k] = base;
   }
-  const int rb = tid >> 2, pb = (tid >> 1) & 1, qb = tid & 1;
-  const uint16_t* bsrc = a.Xhl + (static_cast<size_t>(s_gidx[rb]) * 2 + pb) * dpad + 16 * qb;
-  const int aoff = pa * APL + sa * AP;
-  const int boff = 2 * APL + pb * BPL + rb * AP + 32 * qb;
-  // three stages of loads in flight: stage t lives in register set t % 3 from its issue (two
-  // stages before it is stored to LDS) until its store
-  // register sets are passed by value with named fields (an address-taken or array-member set
-  // is put in scratch, and every copy of a set with loads in flight waits for them)
-  struct ESet {
-    uint4 a0, a1, a2, a3, b0, b1;
-  };
-  auto gload = [&](int s) __attribute__((always_inline)) -> ESet {
-    ESet Rg;
-    const uint4* pa4 = reinterpret_cast<const uint4*>(asrc + KC * s);
-    Rg.a0 = pa4[0];
-    Rg.a1 = pa4[1];
-    Rg.a2 = pa4[2];
-    Rg.a3 = pa4[3];
-    const uint4* p = reinterpret_cast<const uint4*>(bsrc + KC * s);
-    Rg.b0 = p[0];
-    Rg.b1 = p[1];
-    return Rg;
-  };
-  auto lstore = [&](int buf, const ESet Rg) __attribute__((always_inline)) {
-    char* base = sm + buf * STG;
-    uint4* pA = reinterpret_cast<uint4*>(base + aoff);
-    pA[0] = Rg.a0;
-    pA[1] = Rg.a1;
-    pA[2] = Rg.a2;
-    pA[3] = Rg.a3;
-    uint4* pB = reinterpret_cast<uint4*>(base + boff);
-    pB[0] = Rg.b0;
-    pB[1] = Rg.b1;
+  auto issue = [&](int st) __attribute__((always_inline)) {
+    const char* ring = sm + (st % NSTG) * STG;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) dma_piece16(psrc[k] + static_cast<size_t>(st) * (2 * KC), ring + pdst[k]);
   };
 
-  const int S = dpad / KC;
-  // waves w and w+4 share a SIMD: give them different slot groups (ws = w >> 1), so a tile
-  // with few slots (k-means++ rounds) still keeps every SIMD's matrix pipe busy
   const int ws = wave >> 1, wr = wave & 1, lr = lane & 31, hh = lane >> 5;
+  // waves w and w+4 share a SIMD: with ws = w >> 1 they hold different slot groups, so a tile
+  // with few slots (k-means++ rounds) still keeps every SIMD's matrix pipe busy
   const bool wact = 64 * ws < nslots;  // wave-uniform
   v16f acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = v16f{};
-  auto compute = [&](int s) __attribute__((always_inline)) {
+  auto fo = [](int row, int c) { return row * RB + 16 * (c ^ ((row >> 2) & 3)); };
+  auto compute = [&](int st) __attribute__((always_inline)) {
     if (!wact) return;
-    const char* base = sm + (s & 1) * STG;
+    const char* base = sm + (st % NSTG) * STG;
+    // both k-steps' fragments first (16 reads): the second k-step's reads are in flight
+    // under the first k-step's twelve MFMAs
+    h8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      h8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int o = (64 * ws + 32 * i + lr) * AP + 32 * ks + 16 * hh;
-        ah[i] = *reinterpret_cast<const h8*>(base + o);
-        al[i] = *reinterpret_cast<const h8*>(base + APL + o);
+        const int o = fo(64 * ws + 32 * i + lr, 2 * ks + hh);
+        ah[ks][i] = *reinterpret_cast<const h8*>(base + o);
+        al[ks][i] = *reinterpret_cast<const h8*>(base + APL + o);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int o = 2 * APL + (64 * wr + 32 * j + lr) * AP + 32 * ks + 16 * hh;
-        bh[j] = *reinterpret_cast<const h8*>(base + o);
-        bl[j] = *reinterpret_cast<const h8*>(base + BPL + o);
+        const int o = 2 * APL + fo(64 * wr + 32 * j + lr, 2 * ks + hh);
+        bh[ks][j] = *reinterpret_cast<const h8*>(base + o);
+        bl[ks][j] = *reinterpret_cast<const h8*>(base + BPL + o);
       }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          acc[i][j] = mfma16(ah[i], bl[j], acc[i][j]);
-          acc[i][j] = mfma16(al[i], bh[j], acc[i][j]);
-          acc[i][j] = mfma16(ah[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma16(ah[ks][i], bl[ks][j], acc[i][j]);
+          acc[i][j] = mfma16(al[ks][i], bh[ks][j], acc[i][j]);
+          acc[i][j] = mfma16(ah[ks][i], bh[ks][j], acc[i][j]);
         }
-    }
   };
-  ESet R0 = gload(0);
-  lstore(0, R0);
-  ESet R1 = gload(min(1, S - 1));
-  ESet R2 = gload(min(2, S - 1));
-  R0 = gload(min(3, S - 1));
-  __syncthreads();
-  // step s: compute stage s; store stage s+1 (set Rg) to the other buffer; reload Rg with s+4.
-  // Straight-line, every load unconditional (clamped stage index; the extra loads and stores
-  // are never read), so the waits count exactly two younger stages.
-  auto step = [&](int s, const ESet Rg) __attribute__((always_inline)) -> ESet {
-    compute(s);
-    lstore((s + 1) & 1, Rg);
-    __builtin_amdgcn_sched_barrier(0);
-    const ESet Rn = gload(min(s + 4, S - 1));
+  // stage s: wait for its pieces (stage s+1's six may stay in flight), barrier (everyone's
+  // pieces landed, and every wave is done with stage s-1, whose slot the next issue refills),
+  // issue stage s+2, compute stage s
+  issue(0);
+  if (S > 1) issue(1);
+  for (int st = 0; st < S; ++st) {
+    if (st + 1 < S) dma_wait_n<6>();
+    else dma_wait_n<0>();
     __syncthreads();
-    return Rn;
-  };
-  int s = 0;
-  for (; s + 3 <= S; s += 3) {
-    R1 = step(s, R1);
-    R2 = step(s + 1, R2);
-    R0 = step(s + 2, R0);
+    if (st + 2 < S) issue(st + 2);
+    compute(st);
   }
-  if (s < S) R1 = step(s, R1);
-  if (s + 1 < S) R2 = step(s + 1, R2);
+  __syncthreads();
 
   // distance tile D[row][slot] = |c|^2 - 2 x.c (aliases the stages: the loop ended on a barrier)
   float* D = reinterpret_cast<float*>(sm);
