@@ -529,15 +529,24 @@ __device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, i
   const bool eok = (tp >= 0 && tp < T) && erow < m;
   const int w = (tidl >> 6) & 7, hh = (tidl >> 5) & 1;  // tidl is opaque: steps re-read from LDS
   const int ns = __builtin_amdgcn_readfirstlane(S.nsw[w]);
+  // Branch-free over the steps: the step words of all steps are read together (one LDS round
+  // trip per level instead of one per step and level).
+#pragma unroll
+  for (int i = 0; i < NSS; ++i) pre[i] = 0;
+  if (ns == 0) return;  // wave-uniform: Lloyd-only sweeps
+  int its[NSS];
+  unsigned w0s[NSS], w1s[NSS];
+#pragma unroll
+  for (int i = 0; i < NSS; ++i) its[i] = S.sstep[w][i][hh];
 #pragma unroll
   for (int i = 0; i < NSS; ++i) {
-    pre[i] = 0;
-    if (i >= ns) break;
-    const int it = S.sstep[w][i][hh];
-    if (eok && it != 0xFF && iw_kind(S.iw0[it]) == IK_SEED) {
-      const unsigned w1 = S.iw1[it];
-      pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 8) & 7)) * a.lsm + erow]);
-    }
+    w0s[i] = S.iw0[its[i] & (IMAX - 1)];
+    w1s[i] = S.iw1[its[i] & (IMAX - 1)];
+  }
+#pragma unroll
+  for (int i = 0; i < NSS; ++i) {
+    if (i < ns && eok && its[i] != 0xFF && iw_kind(w0s[i]) == IK_SEED)
+      pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(w1s[i] & 31) * T1 + ((w1s[i] >> 8) & 7)) * a.lsm + erow]);
   }
 }
 
@@ -607,13 +616,27 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
   }
   // seeding steps (one item per half-wave)
   const int ns = __builtin_amdgcn_readfirstlane(S.nsw[w]);
+  if (ns == 0) return;  // wave-uniform: Lloyd-only sweeps
+  // step words and distances of all steps first (branch-free: one LDS round trip per level)
+  int its[NSS];
+  unsigned w0s[NSS], w1s[NSS];
+  float dd[NSS];
+#pragma unroll
+  for (int i = 0; i < NSS; ++i) its[i] = S.sstep[w][i][hh];
+#pragma unroll
+  for (int i = 0; i < NSS; ++i) {
+    const bool has = i < ns && its[i] != 0xFF;
+    w0s[i] = has ? S.iw0[its[i] & (IMAX - 1)] : 0u;
+    w1s[i] = has ? S.iw1[its[i] & (IMAX - 1)] : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < NSS; ++i) dd[i] = drow[iw_off(w0s[i])];
 #pragma unroll
   for (int i = 0; i < NSS; ++i) {
     if (i >= ns) break;
-    const int it = S.sstep[w][i][hh];
-    const bool has = it != 0xFF;
-    const unsigned ww = has ? S.iw0[it] : 0u, w1 = has ? S.iw1[it] : 0u;
-    const float dist = fmaxf(xnr + drow[iw_off(ww)], 0.f);
+    const bool has = its[i] != 0xFF;
+    const unsigned ww = w0s[i], w1 = w1s[i];
+    const float dist = fmaxf(xnr + dd[i], 0.f);
     const float dm = (iw_kind(ww) == IK_SEED) ? fminf(__uint_as_float(pre[i]), dist) : dist;
     if (eok && has) {
       dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 11) & 7)) * a.lsm + erow] = dm;
