@@ -56,7 +56,8 @@ constexpr int NBINS = CC_NBINS;
 constexpr int NW = NT / 64;
 // epilogue LDS: hist [NBINS][NT] u32 | 32 edges f32 | wave sums [NBINS][NW] u32 | bin table
 constexpr int BT_OFF = NBINS * NT * 4 + 32 * 4 + NBINS * NW * 4;
-constexpr int BT_MAX_ROWS = (LDS_BYTES - BT_OFF - 16) / ((NBINS + 1) * 2);
+// staged table: rows x 21 uint16 thresholds, then (16-B aligned) rows x f32 reciprocals 20/i
+constexpr int BT_MAX_ROWS = (LDS_BYTES - BT_OFF - 32) / ((NBINS + 1) * 2 + 4);
 static_assert(BT_OFF % 16 == 0, "table copies are 16-B");
 
 __device__ __forceinline__ void tile_coords(int64_t t, int nb, int& bi, int& bj) {
@@ -94,6 +95,15 @@ __device__ __forceinline__ int table_bin(uint32_t m, uint32_t i, const uint16_t*
     g = static_cast<int>(static_cast<float>(m) * (20.0f * __builtin_amdgcn_rcpf(static_cast<float>(i))));
     g = g > NBINS - 1 ? NBINS - 1 : g;
   }
+  const uint16_t* row = tab + i * BT_ROW;
+  return g - (m < row[g] ? 1 : 0) + (m >= row[g + 1] ? 1 : 0);
+}
+
+// table_bin with the reciprocal estimate read from the staged per-row table rtab[i] =
+// 20 * rcp(f32(i)) (rtab[0] = 0): the same g as table_bin, without the convert/rcp/select.
+__device__ __forceinline__ int table_bin_r(uint32_t m, uint32_t i, const uint16_t* tab, const float* rtab) {
+  int g = static_cast<int>(static_cast<float>(m) * rtab[i]);
+  g = g > NBINS - 1 ? NBINS - 1 : g;
   const uint16_t* row = tab + i * BT_ROW;
   return g - (m < row[g] ? 1 : 0) + (m >= row[g + 1] ? 1 : 0);
 }
@@ -225,7 +235,12 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
   const int wr = wave >> 2;  // 0..1 : 128-row half
   const int wc = wave & 3;   // 0..3 : 64-col quarter
   const int nb = (n + T - 1) / T;
-  const int64_t t = tile_begin + blockIdx.x;
+  // XCD-aware tile order: blocks b and b + 8 share an XCD (round-robin dealing), so XCD x gets
+  // the contiguous tile range [x q + min(x, r), ...): its CUs work on neighbouring tiles of one
+  // row band at a time and share the A-side label rows through that XCD's L2.
+  const int nblk = static_cast<int>(gridDim.x), bx = static_cast<int>(blockIdx.x);
+  const int xq = nblk >> 3, xr = nblk & 7, xcd = bx & 7;
+  const int64_t t = tile_begin + xcd * xq + (xcd < xr ? xcd : xr) + (bx >> 3);
   int bi, bj;
   tile_coords(t, nb, bi, bj);
 
@@ -394,9 +409,30 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
       const uint4* src = reinterpret_cast<const uint4*>(btab);
       uint4* dst = reinterpret_cast<uint4*>(tab);
       for (int e = tid; e < vecs; e += NT) dst[e] = src[e];
+      float* rtab = reinterpret_cast<float*>(lds + BT_OFF + 16 * vecs);
+      for (int r = tid; r < bt_rows; r += NT)
+        rtab[r] = r > 0 ? 20.0f * __builtin_amdgcn_rcpf(static_cast<float>(r)) : 0.0f;
     }
     __syncthreads();
+    const float* rtab = reinterpret_cast<const float*>(lds + BT_OFF + 16 * ((bt_rows * BT_ROW * 2 + 15) / 16));
     const uint4* it4 = reinterpret_cast<const uint4*>(I_tiles_in + tl * (T * T) + 128 * tid);
+    // Interior tiles (off the diagonal, every column < n; all but a sliver of the triangle)
+    // bin every element with no pair mask, through the staged reciprocal table.
+    if (btab && !diag && (bj + 1) * T <= n && !full_out) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) {
+          const uint4 q0 = it4[(mi * 2 + nj) * 2], q1 = it4[(mi * 2 + nj) * 2 + 1];
+          const uint32_t iw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const uint32_t ival = (iw[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
+            const int b = table_bin_r(static_cast<uint32_t>(acc[mi][nj][v]), ival, tab, rtab);
+            atomicAdd(&hist[b * NT + tid], 1u);
+          }
+        }
+    } else {
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -420,6 +456,7 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           }
         }
       }
+    }
     // per-bin totals: every thread reads its own counters, a wave sums its 64 lanes into
     // LDS, and 20 threads add the 8 wave sums: one global atomic per bin and tile (20
     // contended words: keep it at one per bin)

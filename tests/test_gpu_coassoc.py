@@ -126,10 +126,11 @@ def test_consensus_matrix_kernel():
     np.testing.assert_array_equal(C, O.consensus_matrix(M.astype(np.uint16), I.astype(np.uint16)))
 
 
-@pytest.mark.parametrize("H,K", [(37, 3), (300, 7), (1000, 20)])
+@pytest.mark.parametrize("H,K", [(37, 3), (256, 10), (300, 7), (1000, 20)])
 def test_threshold_table_binning_is_exact(H, K):
     """cc_coassoc's division-free binning (cc_bin_table thresholds) gives the same 20 counts as
-    the direct numpy-exact bin on every pair; the table itself matches the host oracle's
+    the direct numpy-exact bin on every pair (n = 700: tile (0, 1) takes the interior-tile
+    path with the staged reciprocals, the others the masked path); the table itself matches the host oracle's
     per-pair bin for every (m <= i) it covers."""
     dev = engine.require_gpu()
     n = 700
