@@ -522,6 +522,7 @@ __device__ __forceinline__ int iw_kind(unsigned w) { return (w >> 24) & 3; }
 __device__ __forceinline__ int iw_buf(unsigned w) { return (w >> 30) & 1; }
 
 // Closest distances of the seeding items of tile tp (issued one iteration before its E-step).
+template <int DP>
 __device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, int tp, int T, int tidl,
                                                const float* dbuf, int T1, unsigned (&pre)[NSS]) {
   const int m = a.m;
@@ -529,24 +530,39 @@ __device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, i
   const bool eok = (tp >= 0 && tp < T) && erow < m;
   const int w = (tidl >> 6) & 7, hh = (tidl >> 5) & 1;  // tidl is opaque: steps re-read from LDS
   const int ns = __builtin_amdgcn_readfirstlane(S.nsw[w]);
-  // Branch-free over the steps: the step words of all steps are read together (one LDS round
-  // trip per level instead of one per step and level).
+  if constexpr (DP == 128) {
+    // Branch-free over the steps: the step words of all steps are read together (one LDS
+    // round trip per level instead of one per step and level).  Measured per row width: C3
+    // (d = 128) 2557 -> 2525 ms; at d = 32 / 64 (C5, C2) the same code was 9 % / 4 % slower,
+    // so the narrow instantiations keep the per-step chain.
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) pre[i] = 0;
-  if (ns == 0) return;  // wave-uniform: Lloyd-only sweeps
-  int its[NSS];
-  unsigned w0s[NSS], w1s[NSS];
+    for (int i = 0; i < NSS; ++i) pre[i] = 0;
+    if (ns == 0) return;  // wave-uniform: Lloyd-only sweeps
+    int its[NSS];
+    unsigned w0s[NSS], w1s[NSS];
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) its[i] = S.sstep[w][i][hh];
+    for (int i = 0; i < NSS; ++i) its[i] = S.sstep[w][i][hh];
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) {
-    w0s[i] = S.iw0[its[i] & (IMAX - 1)];
-    w1s[i] = S.iw1[its[i] & (IMAX - 1)];
-  }
+    for (int i = 0; i < NSS; ++i) {
+      w0s[i] = S.iw0[its[i] & (IMAX - 1)];
+      w1s[i] = S.iw1[its[i] & (IMAX - 1)];
+    }
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) {
-    if (i < ns && eok && its[i] != 0xFF && iw_kind(w0s[i]) == IK_SEED)
-      pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(w1s[i] & 31) * T1 + ((w1s[i] >> 8) & 7)) * a.lsm + erow]);
+    for (int i = 0; i < NSS; ++i) {
+      if (i < ns && eok && its[i] != 0xFF && iw_kind(w0s[i]) == IK_SEED)
+        pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(w1s[i] & 31) * T1 + ((w1s[i] >> 8) & 7)) * a.lsm + erow]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NSS; ++i) {
+      pre[i] = 0;
+      if (i >= ns) break;
+      const int it = S.sstep[w][i][hh];
+      if (eok && it != 0xFF && iw_kind(S.iw0[it]) == IK_SEED) {
+        const unsigned w1 = S.iw1[it];
+        pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 8) & 7)) * a.lsm + erow]);
+      }
+    }
   }
 }
 
@@ -616,31 +632,47 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
   }
   // seeding steps (one item per half-wave)
   const int ns = __builtin_amdgcn_readfirstlane(S.nsw[w]);
-  if (ns == 0) return;  // wave-uniform: Lloyd-only sweeps
-  // step words and distances of all steps first (branch-free: one LDS round trip per level)
-  int its[NSS];
-  unsigned w0s[NSS], w1s[NSS];
-  float dd[NSS];
+  if constexpr (DP == 128) {  // see estep_prefetch: branch-free step words at d = 128 only
+    if (ns == 0) return;  // wave-uniform: Lloyd-only sweeps
+    // step words and distances of all steps first (branch-free: one LDS round trip per level)
+    int its[NSS];
+    unsigned w0s[NSS], w1s[NSS];
+    float dd[NSS];
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) its[i] = S.sstep[w][i][hh];
+    for (int i = 0; i < NSS; ++i) its[i] = S.sstep[w][i][hh];
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) {
-    const bool has = i < ns && its[i] != 0xFF;
-    w0s[i] = has ? S.iw0[its[i] & (IMAX - 1)] : 0u;
-    w1s[i] = has ? S.iw1[its[i] & (IMAX - 1)] : 0u;
-  }
+    for (int i = 0; i < NSS; ++i) {
+      const bool has = i < ns && its[i] != 0xFF;
+      w0s[i] = has ? S.iw0[its[i] & (IMAX - 1)] : 0u;
+      w1s[i] = has ? S.iw1[its[i] & (IMAX - 1)] : 0u;
+    }
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) dd[i] = drow[iw_off(w0s[i])];
+    for (int i = 0; i < NSS; ++i) dd[i] = drow[iw_off(w0s[i])];
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) {
-    if (i >= ns) break;
-    const bool has = its[i] != 0xFF;
-    const unsigned ww = w0s[i], w1 = w1s[i];
-    const float dist = fmaxf(xnr + dd[i], 0.f);
-    const float dm = (iw_kind(ww) == IK_SEED) ? fminf(__uint_as_float(pre[i]), dist) : dist;
-    if (eok && has) {
-      dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 11) & 7)) * a.lsm + erow] = dm;
-      es.iaccS[i] += dm;
+    for (int i = 0; i < NSS; ++i) {
+      if (i >= ns) break;
+      const bool has = its[i] != 0xFF;
+      const unsigned ww = w0s[i], w1 = w1s[i];
+      const float dist = fmaxf(xnr + dd[i], 0.f);
+      const float dm = (iw_kind(ww) == IK_SEED) ? fminf(__uint_as_float(pre[i]), dist) : dist;
+      if (eok && has) {
+        dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 11) & 7)) * a.lsm + erow] = dm;
+        es.iaccS[i] += dm;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NSS; ++i) {
+      if (i >= ns) break;
+      const int it = S.sstep[w][i][hh];
+      const bool has = it != 0xFF;
+      const unsigned ww = has ? S.iw0[it] : 0u, w1 = has ? S.iw1[it] : 0u;
+      const float dist = fmaxf(xnr + drow[iw_off(ww)], 0.f);
+      const float dm = (iw_kind(ww) == IK_SEED) ? fminf(__uint_as_float(pre[i]), dist) : dist;
+      if (eok && has) {
+        dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 11) & 7)) * a.lsm + erow] = dm;
+        es.iaccS[i] += dm;
+      }
     }
   }
 }
@@ -964,7 +996,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         if (t + 1 < T) tile_dma<DP>(a, nI, ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * 64, wave, lane);
         if (t + 2 < T) idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
         unsigned npre[NSS];
-        estep_prefetch(a, S, t, T, tidl, dbuf, T1, npre);
+        estep_prefetch<DP>(a, S, t, T, tidl, dbuf, T1, npre);
         KM_STAMP(s1);
         // Stagger: waves w and w+4 share a SIMD; w+4 runs its E-step (VALU) first so that one
         // of the pair issues MFMAs while the other works on the vector pipe.
