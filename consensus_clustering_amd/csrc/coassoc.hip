@@ -457,23 +457,23 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
         }
       }
     }
-    // per-bin totals: every thread reads its own counters, a wave sums its 64 lanes into
-    // LDS, and 20 threads add the 8 wave sums: one global atomic per bin and tile (20
-    // contended words: keep it at one per bin)
-    uint32_t* wsum = reinterpret_cast<uint32_t*>(lds + NBINS * NT * sizeof(uint32_t) + 32 * sizeof(float));
-#pragma unroll
-    for (int b = 0; b < NBINS; ++b) {
-      uint32_t c = hist[b * NT + tid];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-      if (lane == 0) wsum[b * NW + wave] = c;
-    }
+    // per-bin totals: 16 threads per bin sum its 512 counters from LDS (16-B reads, the 16
+    // threads of a bin cover 256 contiguous bytes per read: conflict-free), then reduce
+    // within their 16 lanes: one global atomic per bin and tile (20 contended words: keep it
+    // at one per bin)
     __syncthreads();
-    if (tid < NBINS) {
-      uint32_t sum = 0;
+    if (tid < NBINS * 16) {
+      const int b = tid >> 4, part = tid & 15;
+      const uint4* src = reinterpret_cast<const uint4*>(hist + b * NT) + part;
+      uint32_t c = 0;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) sum += wsum[tid * NW + w];
-      if (sum) atomicAdd(&bin_counts[tid], static_cast<unsigned long long>(sum));
+      for (int k = 0; k < NT / 64; ++k) {
+        const uint4 v = src[16 * k];
+        c += v.x + v.y + v.z + v.w;
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o);
+      if (part == 0 && c) atomicAdd(&bin_counts[b], static_cast<unsigned long long>(c));
     }
   }
 }
