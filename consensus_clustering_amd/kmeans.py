@@ -88,6 +88,14 @@ def choose_subsets(nh: int, n_groups: int, cus: int) -> int:
     return best
 
 
+def default_seedmax(m: int) -> int:
+    """Problems of a unit that may seed (k-means++) concurrently.  Each seeding problem streams
+    closest-distance columns of m rows through HBM every sweep, so the cap shrinks with m.
+    Measured (k-means launch): C3 m = 40k: 10 best of 4..32; C5 m = 160k: 6 -> 464 ms,
+    8 -> 876 ms, 10 -> 898 ms; C2 m = 8k: flat (130-132 ms for 10..32)."""
+    return max(2, min(10, 1_000_000 // max(int(m), 1)))
+
+
 def kpp_tables(Ks, n_init: int, seed: int, m: int, weight_dtype=np.float32):
     """k-means++ streams of RandomState(seed) for each (K, init).
 
@@ -145,14 +153,14 @@ class BatchedKMeans:
     """All (h, K, init) k-means problems of a consensus fit, on one device."""
 
     def __init__(self, Ks, n_init=3, max_iter=300, tol=1e-4, random_state=0,
-                 workspace_budget=8 << 30, seedmax=10, wide_budget=96 << 30):
+                 workspace_budget=8 << 30, seedmax=None, wide_budget=96 << 30):
         self.Ks = [int(k) for k in Ks]
         self.n_init = int(n_init)
         self.max_iter = int(max_iter)
         self.tol = float(tol)
         self.seed = int(random_state)
         self.workspace_budget = int(workspace_budget)
-        self.seedmax = int(seedmax)
+        self.seedmax = None if seedmax is None else int(seedmax)
         self.wide_budget = int(wide_budget)
         self.stats = None
         self.units = None
@@ -177,7 +185,8 @@ class BatchedKMeans:
         u_h = plan(self.Ks, self.n_init, n_sub)
         self.units = u_h
         nU = u_h.shape[0]
-        seedmax = max(1, min(int(os.environ.get("CCMI_SEEDMAX", 0)) or self.seedmax, 32, int(u_h[:, 0].max())))
+        seedmax = max(1, min(int(os.environ.get("CCMI_SEEDMAX", 0)) or self.seedmax or default_seedmax(m),
+                             32, int(u_h[:, 0].max())))
         u, pos, stride = kpp_tables(self.Ks, self.n_init, self.seed, m, weight_dtype)
         u_d = torch.from_numpy(u).to(dev)
         pos_d = torch.from_numpy(pos).to(dev)

@@ -109,6 +109,28 @@ def test_launch_split_is_invariant():
     assert torch.equal(L1, L2)
 
 
+def test_seeding_cap_is_invariant():
+    """The cap on concurrently seeding problems (default_seedmax) only changes how sweeps are
+    packed, never a label."""
+    dev = engine.require_gpu()
+    X = blobs(900, 24, 5, seed=5)
+    n, d = X.shape
+    Ks, H, m = [2, 3, 5, 7, 9], 6, 720
+    idx = engine.resample_indices(7, n, m, 0, H)
+    idx_d = torch.from_numpy(idx).to(dev)
+    Xd, xn, _, Xhl, e = prepare_rows(X, dev)
+    kw = dict(Xhl=Xhl, scale_exp=e)
+    ref = None
+    for cap in (1, 3, 10, 32):
+        L = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
+        BatchedKMeans(Ks, random_state=7, seedmax=cap).run(Xd, xn, d, idx_d, n, H, m, 0, H, L, np.float32, **kw)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = L
+        else:
+            assert torch.equal(ref, L), f"seedmax={cap}"
+
+
 def test_wide_batching_is_invariant():
     """Wide rows: the resample batch size (workspace budget) and launch split change nothing."""
     dev = engine.require_gpu()
