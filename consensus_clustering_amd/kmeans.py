@@ -91,9 +91,10 @@ def choose_subsets(nh: int, n_groups: int, cus: int) -> int:
 def default_seedmax(m: int) -> int:
     """Problems of a unit that may seed (k-means++) concurrently.  Each seeding problem streams
     closest-distance columns of m rows through HBM every sweep, so the cap shrinks with m.
-    Measured (k-means launch): C3 m = 40k: 10 best of 4..32; C5 m = 160k: 6 -> 464 ms,
-    8 -> 876 ms, 10 -> 898 ms; C2 m = 8k: flat (130-132 ms for 10..32)."""
-    return max(2, min(10, 1_000_000 // max(int(m), 1)))
+    Measured (k-means launch): C3 m = 40k: 6 / 8 / 10 / 12 / 14 / 16 / 20 -> 2692 / 2576 /
+    2530 / 2512 / 2517 / 2542 / 2555 ms; C5 m = 160k: 6 -> 464 ms, 8 -> 876 ms, 10 -> 898 ms;
+    C2 m = 8k: flat (130-132 ms for 10..32)."""
+    return max(2, min(12, 1_000_000 // max(int(m), 1)))
 
 
 def kpp_tables(Ks, n_init: int, seed: int, m: int, weight_dtype=np.float32):
