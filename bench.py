@@ -49,6 +49,7 @@ CONFIGS = {
 # the algorithmic (f32-equivalent) flops of the k-means is a third of it.
 F16_MFMA_PEAK_TF = 2516.6
 KMEANS_PEAK_TF = F16_MFMA_PEAK_TF / 3
+I8_MFMA_PEAK_TOPS = 2 * F16_MFMA_PEAK_TF  # v_mfma_i32_32x32x32_i8: 2x the f16 rate
 SEED = 0
 
 
@@ -75,60 +76,104 @@ def make_expression_f32(n, d, groups=5, informative=500, shift_std=2.0, seed=0):
     return X
 
 
-def cpu_baseline(cfg, X, budget_s=25.0):
-    """Reference algorithm (oracle: numpy + sklearn) on a bounded sample, extrapolated.
-
-    Per (h, K) the reference does a KMeans fit of X[idx_h] (CC.py:282) and the one-hot
-    co-association M += LᵀL on n x n uint16 (CC.py:284-290).  We time fits for a few K and
-    LᵀL + add on a row block of the n x n product, then extrapolate linearly in K and in
-    rows: T(h,K) = t_fit(K) + t_coassoc(K); T = Σ_K H·T(h,K).
-    """
+def _timed_fit(X, idx_row, K):
+    """One reference fit (CC.py:282, sklearn KMeans n_init=3) on one BLAS/OpenMP thread."""
     from threadpoolctl import threadpool_limits
 
     from oracle import cc_oracle as O
 
-    n, H = cfg["n"], cfg["H"]
-    m = int(cfg["frac"] * n)
+    with threadpool_limits(1):
+        t = time.perf_counter()
+        O.kmeans_labels(X[idx_row], K, SEED, n_init=3)
+        return time.perf_counter() - t
+
+
+def _timed_coassoc(n, idx_row, lab_seed, K, block):
+    """CC.py:284-290 for one (h, K) on a `block`-row slice of the n x n uint16 M: one-hot L,
+    the integer L^T L and the in-place add (one thread)."""
+    from threadpoolctl import threadpool_limits
+
+    rs = np.random.RandomState(lab_seed)
+    lab = rs.randint(0, K, size=len(idx_row))
+    with threadpool_limits(1):
+        L = np.zeros((K, n), dtype=np.uint16)
+        L[lab, idx_row] = 1
+        Mblk = np.zeros((block, n), dtype=np.uint16)
+        t = time.perf_counter()
+        Mblk += np.dot(L[:, :block].T, L)
+        return time.perf_counter() - t
+
+
+def cpu_baseline(cfg, X, H_sample=8):
+    """The reference's parallelised CPU path (CC.py:162-199, joblib processes, n_jobs = the
+    box's CPU share) timed on a bounded sample of the same workload and
+    extrapolated linearly in H:
+
+      T = T_I(H) + Σ_K [H / H' · T_fits(K, H')] + Σ_K H · t_co(K) / n_jobs + Σ_K t_an(K)
+
+    * T_fits: all K, H' resamples, every KMeans fit a joblib process task with one BLAS thread;
+    * t_co(K): one (h, K) co-association (one-hot L^T L + in-place add, CC.py:284-290) timed on
+      a row block and scaled to n rows, for 3 sampled K and interpolated (the reference runs
+      these inside the same n_jobs workers);
+    * T_I: the integer S^T S (CC.py:264) and t_an: C = M / I + histogram (CC.py:338-373), both
+      serial in the reference, timed on row blocks and scaled to n rows.
+    """
+    from joblib import Parallel, delayed
+    from threadpoolctl import threadpool_limits
+
+    from oracle import cc_oracle as O
+
+    n, H, frac = cfg["n"], cfg["H"], cfg["frac"]
     Ks = cfg["Ks"]
     cores = min(16, os.cpu_count() or 1)
-    idx = O.subsampling_indices(n, 1, cfg["frac"], SEED)
-    sampleK = sorted({Ks[0], Ks[len(Ks) // 2], Ks[-1]})
-    t_fit, t_co = {}, {}
-    block = min(n, 2000)
+    Hs = min(H, H_sample)
+    idx = O.subsampling_indices(n, Hs, frac, SEED)
     t0 = time.perf_counter()
-    with threadpool_limits(cores):
-        for K in sampleK:
-            a = time.perf_counter()
-            lab = O.kmeans_labels(X[idx[0]], K, SEED, n_init=3)
-            t_fit[K] = time.perf_counter() - a
-            L = np.zeros((K, n), dtype=np.uint16)
-            L[lab, idx[0]] = 1
-            Mblk = np.zeros((block, n), dtype=np.uint16)
-            a = time.perf_counter()
-            mij = np.dot(L[:, :block].T, L)   # CC.py:287 on a row block
-            Mblk += mij                        # CC.py:290
-            t_co[K] = (time.perf_counter() - a) * (n / block)
-            if time.perf_counter() - t0 > budget_s:
-                break
-    done = sorted(t_fit)
-    per_K = {K: np.interp(K, done, [t_fit[k] + t_co[k] for k in done]) for K in Ks}
-    total = H * sum(per_K.values())
+    with Parallel(n_jobs=cores, prefer="processes") as par:
+        a = time.perf_counter()
+        par(delayed(_timed_fit)(X, idx[h], K) for K in Ks for h in range(Hs))
+        T_fits = (time.perf_counter() - a) * (H / Hs)
+        block = min(n, 1000)
+        sampleK = sorted({Ks[0], Ks[len(Ks) // 2], Ks[-1]})
+        tco = par(delayed(_timed_coassoc)(n, idx[0], K, K, block) for K in sampleK)
+    t_co = {K: t * (n / block) for K, t in zip(sampleK, tco)}
+    T_co = sum(H * np.interp(K, sampleK, [t_co[k] for k in sampleK]) for K in Ks) / cores
+    # I = S^T S (serial numpy integer matmul) and the per-K analysis, on row blocks
+    with threadpool_limits(1):
+        bI = min(n, 200)
+        S = (np.random.RandomState(0).rand(H, n) < frac).astype(np.uint16 if H >= 256 else np.uint8)
+        a = time.perf_counter()
+        np.dot(S[:, :bI].T, S)
+        T_I = (time.perf_counter() - a) * (n / bI)
+        bA = min(n, 500)
+        M = np.random.RandomState(1).randint(0, H + 1, size=(bA, n), dtype=S.dtype)
+        I = np.maximum(M, H // 2).astype(S.dtype)
+        a = time.perf_counter()
+        C = np.divide(M, I + 1e-6, dtype=np.float32)
+        np.histogram(np.triu(C, k=1).ravel(), bins=20, range=(0, 1), density=True)
+        T_an = (time.perf_counter() - a) * (n / bA) * len(Ks)
+    total = T_I + T_fits + T_co + T_an
     return {
         "value": H * len(Ks) / total,
         "unit": "resample-clusterings/s",
         "cores": cores,
         "kind": "port",
-        "sample": (f"oracle (numpy + sklearn {__import__('sklearn').__version__} KMeans n_init=3) "
-                   f"on resample 0 for K in {done}: KMeans fit + one-hot LᵀL/add on a {block}-row "
-                   f"block of the {n}x{n} uint16 M, scaled x{n / block:.0f} in rows, "
-                   f"interpolated over K={Ks[0]}..{Ks[-1]}, x H={H}; extrapolated fit "
-                   f"{total / 3600:.1f} h; sampled {time.perf_counter() - t0:.1f} s"),
+        "sample": (f"reference algorithm (oracle: numpy {np.__version__} + sklearn "
+                   f"{__import__('sklearn').__version__} KMeans n_init=3), joblib processes "
+                   f"n_jobs={cores} x 1 BLAS thread (CC.py:185-195): all {len(Ks)} K x H'={Hs} "
+                   f"resample fits timed ({T_fits * Hs / H:.1f} s wall), extrapolated x{H / Hs:.0f} "
+                   f"in H; co-association L^T L + add timed on a {block}-row block for K in "
+                   f"{sampleK} and scaled to n rows / n_jobs; S^T S ({bI}-row block) and "
+                   f"C/histogram ({bA}-row block) serial, scaled to n rows. Extrapolated fit "
+                   f"{total / 3600:.2f} h = I {T_I:.0f} s + fits {T_fits:.0f} s + co-association "
+                   f"{T_co:.0f} s + analysis {T_an:.0f} s; sampled {time.perf_counter() - t0:.1f} s"),
     }
 
 
-def load_traffic(prefix="profiles"):
-    """Per-launch HBM bytes of cc_kmeans_batched from a committed PMC summary, if present."""
-    path = os.path.join(ROOT, prefix, "kmeans_traffic.json")
+def load_traffic(config, kernel, prefix="profiles"):
+    """Per-launch HBM bytes of `kernel` at `config` from a committed PMC summary
+    (profiles/traffic/<config>_<kernel>.json), or None when no such measurement exists."""
+    path = os.path.join(ROOT, prefix, "traffic", f"{config}_{kernel}.json")
     if os.path.exists(path):
         with open(path) as f:
             return json.load(f).get("bytes_per_launch")
@@ -143,6 +188,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--H", type=int, default=None, help="override n_iterations (debug runs)")
+    ap.add_argument("--rehearse", default=None, metavar="R/N",
+                    help="one-GPU rehearsal of rank R's share of an N-GPU fit (exchanges skipped; "
+                         "the fit's results are partial, the timing is rank R's critical path)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.H:
@@ -167,6 +215,9 @@ def main():
     Xd = torch.from_numpy(X).to(dev)  # inputs resident in HBM before the timed region
     cc = ConsensusClustering(K_range=cfg["Ks"], n_iterations=cfg["H"], subsampling=cfg["frac"],
                              random_state=SEED, plot_cdf=False, keep_matrices=False)
+    if args.rehearse:
+        r, w = (int(v) for v in args.rehearse.split("/"))
+        cc._rehearsal = (r, w)
 
     def barrier():
         if world > 1:
@@ -198,7 +249,8 @@ def main():
     st = stats.to(torch.float64)
     km_kernel = "cc_kmeans_batched" if cfg["d"] <= 128 else "cc_kmeans_wide"
     km_launch, km_ms = timers.get(km_kernel, (0, 0.0))
-    ktime = torch.tensor([km_ms, float(km_launch)], dtype=torch.float64, device=dev)
+    co_launch, co_ms = timers.get("cc_coassoc", (0, 0.0))
+    ktime = torch.tensor([km_ms, float(km_launch), co_ms], dtype=torch.float64, device=dev)
     if world > 1:
         tdist.all_reduce(vec, op=tdist.ReduceOp.MAX)
         tdist.all_reduce(st, op=tdist.ReduceOp.SUM)
@@ -210,9 +262,15 @@ def main():
     achieved = flops / (km_ms_tot * 1e-3) / 1e12 if km_ms_tot > 0 else 0.0
     clusterings = cfg["H"] * len(cfg["Ks"]) * args.steps
     value = clusterings / elapsed
+    # co-association: OPS_M = sum_K 2 P H K per fit (channel padding and the
+    # diagonal tiles' lower halves not credited) over the HIP-event time of its launches
+    P = cfg["n"] * (cfg["n"] - 1) / 2
+    co_ops = sum(2.0 * P * cfg["H"] * K for K in cfg["Ks"]) * args.steps
+    co_ms_tot = float(ktime[2])
+    co_achieved = co_ops / (co_ms_tot * 1e-3) / 1e12 if co_ms_tot > 0 else 0.0
 
     if rank == 0:
-        traffic = load_traffic()
+        traffic = load_traffic(args.config, km_kernel)
         out = {
             "metric": METRIC,
             "value": value,
@@ -245,9 +303,22 @@ def main():
                 "flops_per_launch": flops / km_launches,
                 "avg_launch_ms": km_ms_tot / km_launches,
             },
+            "roofline_coassoc": {
+                "kernel": "cc_coassoc",
+                "bound": "mfma",
+                "achieved": co_achieved,
+                "peak": I8_MFMA_PEAK_TOPS,
+                "unit": "TOP/s",
+                "frac": co_achieved / I8_MFMA_PEAK_TOPS,
+                "ops_per_fit": co_ops / args.steps,
+                "ms_per_fit": co_ms_tot / args.steps,
+                "traffic": load_traffic(args.config, "cc_coassoc"),
+                "note": "the 20-bin histogram (K5) is fused into this kernel's epilogue: no HBM pass",
+            },
             "kernels_ms_per_step": {k: v[1] / args.steps for k, v in timers.items()},
             "kernel_launches_per_step": {k: v[0] / args.steps for k, v in timers.items()},
             "fit_timings_s": {k: round(v, 4) for k, v in cc.timings_.items()},
+            "partial": bool(cc.partial_),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, X)

@@ -8,6 +8,7 @@ raises, so a run can never silently measure or validate a CPU path.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import threading
 
@@ -43,7 +44,27 @@ SIGNATURES = {
     "cc_kmeans_wide": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int,
                                 _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_dbl, _vp, _c_int,
                                 _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_sz, _c_int, _vp]),
+    "cc_build_id": (ctypes.c_char_p, []),
+    "cc_bin_selftest": (_c_int, [_c_int, _vp, _vp, _vp, _vp]),
+    "cc_manhattan": (_c_int, [_vp, _c_int, _c_int, _vp, _vp]),
+    "cc_kmeans_f64_workspace_bytes": (_c_sz, [_c_int, _c_int, _vp, _c_int, _c_int]),
+    "cc_kmeans_f64": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp,
+                               _c_int, _c_int, _c_int, _c_dbl, _vp, _c_int, _vp, _vp, _c_int, _vp,
+                               _vp, _vp, _c_sz, _c_int, _vp]),
 }
+
+_CSRC = os.path.join(_HERE, "csrc")
+_INCLUDE = os.path.join(os.path.dirname(_HERE), "include", "ccmi.h")
+
+
+def source_build_id() -> str:
+    """The build id the csrc Makefile embeds: SHA-256 prefix over the sources in its order."""
+    names = sorted(f for f in os.listdir(_CSRC) if f.endswith((".hip", ".cpp", ".h", ".hpp")))
+    h = hashlib.sha256()
+    for path in [os.path.join(_CSRC, f) for f in names] + [_INCLUDE, os.path.join(_CSRC, "Makefile")]:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 _lock = threading.Lock()
 _lib = None
@@ -68,6 +89,17 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        # provenance: the library must be built from exactly the sources next to it, with the
+        # default flags (no diagnostic -D variant), unless CCMI_LIB names one explicitly
+        if "CCMI_LIB" not in os.environ and os.path.isdir(_CSRC):
+            built = lib.cc_build_id().decode()
+            want = source_build_id()
+            if built != want:
+                raise CCMIError(
+                    f"stale libccmi.so (built from {built}, sources are {want}): rebuild with "
+                    "`make -C consensus_clustering_amd/csrc` or __graft_entry__.build()")
+            if b"-D" in lib.cc_version():
+                raise CCMIError("libccmi.so is a diagnostic build (-D flags): rebuild it")
         _lib = lib
         return lib
 

@@ -27,12 +27,15 @@ Additions: ``cdf_area_``, ``delta_k_``, ``pac_area_``, ``best_k_`` and ``predict
 from __future__ import annotations
 
 import time
+import warnings
 
 import numpy as np
 import torch
 
 from . import dist, engine, post
 from .kmeans import BatchedKMeans
+
+KMAX = 127  # largest K: uint8 labels (0xFF = not sampled) and int8 one-hot channels
 
 
 def _default_kmeans():
@@ -77,6 +80,7 @@ class ConsensusClustering:
         keep_matrices='auto',
         device=None,
         workspace_budget=8 << 30,
+        precision='auto',
     ):
         self.K_range = K_range
         self.n_iterations = n_iterations
@@ -97,7 +101,11 @@ class ConsensusClustering:
         self.keep_matrices = keep_matrices
         self.device = device
         self.workspace_budget = workspace_budget
+        # k-means arithmetic: 'f64' = float64 like sklearn on float64 input (cc_kmeans_f64),
+        # 'fast' = the float32-class f16 hi/lo MFMA engine; 'auto' picks by the input dtype
+        self.precision = precision
         self.timings_ = {}
+        self._rehearsal = None  # (rank, world): bench tooling only, see fit()
 
         if self.clusterer is None:
             print('KMeans is set as default clusterer')
@@ -144,7 +152,17 @@ class ConsensusClustering:
         n, H = self._N, int(self.n_iterations)
         m = int(self.subsampling * n)
         Ks = [int(K) for K in self.K_range]
+        self._check_k_range(Ks)
         rank, W = dist.world()
+        self.partial_ = False
+        if self._rehearsal is not None:
+            # one-GPU rehearsal of rank r's share of a W-rank fit (bench tooling only): the
+            # exchanges are skipped, so every count below covers rank r's share alone
+            if W > 1:
+                raise RuntimeError("rehearsal runs without a process group")
+            rank, W = self._rehearsal
+            self.partial_ = True
+            warnings.warn(f"rehearsing rank {rank} of {W}: results are PARTIAL (timing only)")
         dev = engine.require_gpu(self.device)
         keep = self.keep_matrices
         if keep == 'auto':
@@ -160,16 +178,30 @@ class ConsensusClustering:
 
         km = self._kmeans_params()
         self.backend_ = 'gpu-kmeans' if km is not None else 'host-clusterer'
+        precision = self.precision
+        if precision == 'auto':
+            precision = 'f64' if wdtype == np.float64 else 'fast'
+        if precision not in ('f64', 'fast'):
+            raise ValueError("precision must be 'auto', 'f64' or 'fast'")
+        self.precision_ = precision if km is not None else None
         if Ks and km is not None:
-            Xd, xnorm, _, Xhl, sexp = _prepare(X, dev)
             bk = BatchedKMeans(Ks, n_init=km["n_init"], max_iter=km["max_iter"], tol=km["tol"],
                                random_state=self.random_state,
                                workspace_budget=self.workspace_budget)
-            self.kmeans_inertia_ = torch.zeros((len(Ks), H), dtype=torch.float32, device=dev)
             self.kmeans_n_iter_ = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
-            bk.run(Xd, xnorm, X.shape[1], idx_d, n, H, m, h0, h1, labels, weight_dtype=wdtype,
-                   inertia=self.kmeans_inertia_, n_iter=self.kmeans_n_iter_, Xhl=Xhl,
-                   scale_exp=sexp)
+            if precision == 'f64':
+                # float64 input: the reference's clusterer runs in float64 (CC.py:282)
+                X64 = (X.to(dev, torch.float64) if isinstance(X, torch.Tensor)
+                       else torch.from_numpy(np.ascontiguousarray(X, dtype=np.float64)).to(dev))
+                self.kmeans_inertia_ = torch.zeros((len(Ks), H), dtype=torch.float64, device=dev)
+                bk.run_f64(X64.contiguous(), idx_d, n, H, m, h0, h1, labels,
+                           inertia=self.kmeans_inertia_, n_iter=self.kmeans_n_iter_)
+            else:
+                Xd, xnorm, _, Xhl, sexp = _prepare(X, dev)
+                self.kmeans_inertia_ = torch.zeros((len(Ks), H), dtype=torch.float32, device=dev)
+                bk.run(Xd, xnorm, X.shape[1], idx_d, n, H, m, h0, h1, labels, weight_dtype=wdtype,
+                       inertia=self.kmeans_inertia_, n_iter=self.kmeans_n_iter_, Xhl=Xhl,
+                       scale_exp=sexp)
             self.kmeans_stats_ = bk.stats
         elif Ks:
             if isinstance(X, torch.Tensor):
@@ -180,8 +212,8 @@ class ConsensusClustering:
                 lab = np.empty((h1 - h0, m), dtype=np.int32)
                 for h in range(h0, h1):
                     lab[h - h0] = np.asarray(self.clusterer.fit_predict(X[idx[h]]))
-                if lab.size and (lab.min() < 0 or lab.max() >= min(K, 128)):
-                    raise ValueError(f"clusterer labels must lie in [0, {K}) and K <= 127")
+                if lab.size and (lab.min() < 0 or lab.max() >= K):
+                    raise ValueError(f"clusterer labels must lie in [0, {K})")
                 engine.scatter_labels(idx_d[h0:h1].contiguous(), torch.from_numpy(lab).to(dev), n,
                                       labels[k], h_offset=h0)
         dist.merge_labels(labels)
@@ -231,6 +263,13 @@ class ConsensusClustering:
         if self.plot_cdf and rank == 0:
             self._plot_cdf()
         return self
+
+    def _check_k_range(self, Ks):
+        """Every K of K_range must be an integer in [1, 127] (the uint8 label format and the
+        int8 co-association), checked before any clustering runs."""
+        for K in Ks:
+            if K < 1 or K > KMAX:
+                raise ValueError(f"K_range values must lie in [1, {KMAX}], got {K}")
 
     def _finish_selection(self):
         d = self.cdf_at_K_data
@@ -288,36 +327,68 @@ class ConsensusClustering:
             out[K] = path
         return out
 
-    def predict(self, K=None):
-        """Consensus labels: average-linkage agglomerative clustering of 1 - C for K
-        (default best_k_).  The reference's `_get_consensus_labels` (CC.py:292-314) is
-        dead code that no longer runs on sklearn >= 1.4; this uses the same linkage on
-        the precomputed consensus distance."""
+    # largest n for predict(): the linkage runs on the host over the n x n float64 distances
+    PREDICT_MAX_N = 20000
+
+    def predict(self, K=None, distance='manhattan'):
+        """Consensus labels for K (default ``best_k_``).
+
+        distance='manhattan' (default) is the reference's intended semantics
+        (`_get_consensus_labels`, CC.py:292-314): agglomerative clustering with
+        ``agg_clustering_linkage`` of the ROWS of C under the manhattan metric
+        (``AgglomerativeClustering(n_clusters=K, linkage=..., affinity='manhattan')``, CC.py:306-312;
+        sklearn >= 1.4 spells the keyword ``metric``).  The n x n manhattan distances are
+        computed on the GPU in float64 with scipy's summation order (cc_manhattan, bit-identical
+        to ``scipy.spatial.distance.pdist(C, 'cityblock')``), then the linkage runs on the host.
+
+        distance='1-C' is an opt-in variant: the same linkage over 1 - C as a precomputed
+        consensus distance.
+
+        The host linkage needs O(n^2) float64 memory, so n is capped at PREDICT_MAX_N.
+        """
         from sklearn.cluster import AgglomerativeClustering
 
         K = self.best_k_ if K is None else K
+        n = self._N
+        if n > self.PREDICT_MAX_N:
+            raise ValueError(f"predict(): n = {n} > PREDICT_MAX_N = {self.PREDICT_MAX_N}; the "
+                             "host linkage needs n^2 float64 distances")
+        if self.agg_clustering_linkage == 'ward':
+            raise ValueError("ward linkage needs the euclidean metric; the reference's manhattan "
+                             "consensus linkage supports 'average', 'complete' and 'single'")
         C = self.consensus_matrix(K)
+        if distance == 'manhattan':
+            D = engine.manhattan(torch.from_numpy(np.ascontiguousarray(C)).to(self.labels_.device))
+            D = D.cpu().numpy()
+        elif distance == '1-C':
+            D = 1.0 - C.astype(np.float64)
+        else:
+            raise ValueError("distance must be 'manhattan' or '1-C'")
         agg = AgglomerativeClustering(n_clusters=K, metric='precomputed',
                                       linkage=self.agg_clustering_linkage)
-        return agg.fit_predict(1.0 - C.astype(np.float64))
+        return agg.fit_predict(D)
 
-    def _plot_cdf(self):
-        """CC.py:389-410 (presentation only)."""
+    def _plot_cdf(self, ax=None):
+        """Consensus CDF per K as a step curve over the bin upper edges, with the PAC interval
+        shaded (the ``plot_cdf`` option of CC.py:133-134; presentation only, host matplotlib).
+        Returns the axes, or None when matplotlib is not installed."""
         try:
             import matplotlib.pyplot as plt
         except ImportError:  # pragma: no cover
-            return
-        plt.figure(figsize=(4, 4), dpi=120)
-        for K, data in self.cdf_at_K_data.items():
-            x = data['bin_edges']
-            y = [0] + [v for v in data['cdf']]
-            plt.plot(x, y, marker='o', markersize=2.5, label=f'K: {K}', linewidth=2.0)
-        plt.vlines(self.PAC_interval, *plt.ylim(), colors='k', linestyles='dashed', lw=1.5)
-        plt.xlabel('consensus index value')
-        plt.ylabel('CDF')
-        plt.legend()
-        plt.tight_layout()
-        plt.show()
+            return None
+        if ax is None:
+            ax = plt.gca()
+        lo, hi = self.PAC_interval
+        ax.axvspan(lo, hi, color='0.9', zorder=0)
+        for K, res in self.cdf_at_K_data.items():
+            upper = np.asarray(res['bin_edges'][1:], dtype=np.float64)
+            ax.step(upper, res['cdf'], where='post', label=f'K={K} (PAC {float(res["pac_area"]):.3f})')
+        ax.set_xlim(0.0, 1.0)
+        ax.set_ylim(0.0, 1.02)
+        ax.set_xlabel('consensus value')
+        ax.set_ylabel('fraction of pairs <= value')
+        ax.legend(fontsize='small')
+        return ax
 
 
 def _prepare(X, dev):

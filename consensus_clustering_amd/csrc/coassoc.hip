@@ -129,6 +129,28 @@ __global__ void bin_table_kernel(int rows, const float* __restrict__ edges, uint
   table[e] = static_cast<uint16_t>(t);
 }
 
+// Exhaustive check of the division-free binning: for every pair (m <= i < rows) compare
+// table_bin and table_bin_r (with the epilogue's own reciprocal 20 * rcp(i)) against the direct
+// numpy-exact consensus_bin; mismatches[0] / [1] count the disagreements of the two forms.
+__global__ void bin_selftest_kernel(int rows, const float* __restrict__ edges,
+                                    const uint16_t* __restrict__ table,
+                                    unsigned long long* __restrict__ mismatches) {
+  const int i = blockIdx.x;
+  const float rt = i > 0 ? 20.0f * __builtin_amdgcn_rcpf(static_cast<float>(i)) : 0.0f;
+  __shared__ float rtab_i[1];
+  if (threadIdx.x == 0) rtab_i[0] = rt;
+  __syncthreads();
+  unsigned long long bad0 = 0, bad1 = 0;
+  for (int m = threadIdx.x; m <= i; m += blockDim.x) {
+    const int want = consensus_bin(static_cast<uint32_t>(m), static_cast<uint32_t>(i), edges);
+    bad0 += table_bin(static_cast<uint32_t>(m), static_cast<uint32_t>(i), table) != want;
+    // table_bin_r reads rtab[i]: point it at a one-entry array holding row i's reciprocal
+    bad1 += table_bin_r(static_cast<uint32_t>(m), static_cast<uint32_t>(i), table, rtab_i - i) != want;
+  }
+  if (bad0) atomicAdd(&mismatches[0], bad0);
+  if (bad1) atomicAdd(&mismatches[1], bad1);
+}
+
 // Load the HS = 128/KP label bytes of one row for one super-step into w[].
 // Branch-free: an out-of-range row reads row 0 and is masked to 0xFF (= not sampled).
 template <int KP>
@@ -593,6 +615,17 @@ extern "C" int cc_bin_table(int rows, const float* edges, uint16_t* table, void*
 }
 
 extern "C" int cc_bin_table_max_rows(void) { return BT_MAX_ROWS; }
+
+extern "C" int cc_bin_selftest(int rows, const float* edges, const uint16_t* table,
+                               unsigned long long* mismatches, void* stream) {
+  if (rows <= 0 || rows > BT_MAX_ROWS || !edges || !table || !mismatches) {
+    cc::set_error("cc_bin_selftest: bad arguments (1 <= rows <= cc_bin_table_max_rows())");
+    return CC_ERR_ARG;
+  }
+  hipLaunchKernelGGL(bin_selftest_kernel, dim3(rows), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     rows, edges, table, mismatches);
+  return launch_status("cc_bin_selftest");
+}
 
 extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int K,
                           int64_t tile_begin, int64_t tile_end, const uint16_t* I_tiles,

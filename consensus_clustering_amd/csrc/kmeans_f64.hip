@@ -1,0 +1,589 @@
+// Float64 k-means for float64 input: the reference's clusterer at the reference's precision.
+//
+// The reference clusters whatever dtype X has (CC.py:282; its notebook and BASELINE config 1
+// pass float64 `.values`), and scikit-learn's KMeans then runs in float64.  The f16 hi/lo MFMA
+// engine (kmeans.hip) is float32-class; this kernel is the float64 path.  It restates
+// scikit-learn 1.7 (sklearn/cluster/_kmeans.py, _k_means_lloyd.pyx, _k_means_common.pyx)
+// operation by operation in float64, with its reduction orders where they are sequential:
+//   * X_sub centred by its own column means (KMeans.fit, :1479-1481; rows summed in order);
+//   * tol = mean(var(X_sub, axis=0)) * tol_rel (_tolerance; numpy pairwise mean over features);
+//   * k-means++ (_kmeans_plusplus): squared distances ((-2 x.c) + |c|^2) + |x|^2 clipped at 0
+//     (_euclidean_distances), candidates by searchsorted over the float64 cumsum, the
+//     candidate with the lowest potential kept;
+//   * Lloyd (_kmeans_single_lloyd / lloyd_iter_chunked_dense): distances |c|^2 - 2 x.c,
+//     argmin with strict < (lowest index on ties), centre sums in row order, empty clusters
+//     relocated to the farthest points, averaging with 1/weight, shifts by the 4-way unrolled
+//     _euclidean_dense_dense, strict convergence else sum(shift^2) <= tol, a final E-step when
+//     not strictly converged, inertia summed in row order;
+//   * best of n_init: lower inertia and a different clustering (_is_same_clustering).
+// Dot products are sequential fused multiply-adds over the features (the BLAS micro-kernel
+// order); float contraction is otherwise off, as in the reference's compiled Cython.
+//
+// Mapping: a persistent grid; one 256-thread workgroup runs one (resample, K) unit at a time
+// (all its inits, sequentially), with per-workgroup float64 scratch in the caller's workspace.
+// It is the precision path for float64 input, not the throughput path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <string>
+
+#include "ccmi_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int KMAX = 127;
+constexpr int TMAX = 6;
+constexpr int NKMAX = 64;
+
+struct F64Args {
+  const double* X;  // [n][d] (not centred)
+  int n, d;
+  const int32_t* idx;  // [H][m]
+  int H, m, h_begin, nh;
+  int nK;
+  int Ks[NKMAX];
+  int n_init, max_iter;
+  double tol_rel;
+  const double* kpp_u;  // [nK][n_init][stride]
+  int kpp_stride;
+  const int32_t* kpp_pos;  // [nK][n_init]
+  uint8_t* labels;         // [nK][n][ldl]
+  int ldl;
+  double* inertia_out;  // [nK][H] or null
+  int32_t* niter_out;   // [nK][H] or null
+  unsigned* counter;
+  char* ws;
+  size_t per_wg;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest;
+};
+
+// numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) of a contiguous double array:
+// sequential below 8, eight interleaved partial sums up to 128, else split at
+// floor(n / 2) rounded down to a multiple of 8 and recurse.
+__device__ double np_pairwise(const double* a, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise(a, n2) + np_pairwise(a + n2, n - n2);
+}
+
+// _euclidean_dense_dense (squared): 4-way unrolled, left to right
+__device__ __forceinline__ double euclid4(const double* a, const double* b, int d) {
+  double res = 0.0;
+  const int n4 = d / 4, rem = d % 4;
+  for (int i = 0; i < n4; ++i) {
+    const double d0 = a[4 * i] - b[4 * i], d1 = a[4 * i + 1] - b[4 * i + 1];
+    const double d2 = a[4 * i + 2] - b[4 * i + 2], d3 = a[4 * i + 3] - b[4 * i + 3];
+    res += ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;
+  }
+  for (int i = 0; i < rem; ++i) {
+    const double t = a[4 * n4 + i] - b[4 * n4 + i];
+    res += t * t;
+  }
+  return res;
+}
+
+struct WG {
+  double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew;
+  int32_t *lab, *lold;
+  uint8_t* lbest;
+};
+
+// centred feature k of resample row r
+__device__ __forceinline__ double xc(const F64Args& a, const int32_t* idx, const double* mean, int r, int k) {
+  return a.X[static_cast<size_t>(idx[r]) * a.d + k] - mean[k];
+}
+
+__device__ double dotc(const F64Args& a, const int32_t* idx, const double* mean, int r, const double* c) {
+  double s = 0.0;
+  for (int k = 0; k < a.d; ++k) s = __fma_rn(xc(a, idx, mean, r, k), c[k], s);
+  return s;
+}
+
+__device__ double dotrr(const F64Args& a, const int32_t* idx, const double* mean, int r, int q) {
+  double s = 0.0;
+  for (int k = 0; k < a.d; ++k) s = __fma_rn(xc(a, idx, mean, r, k), xc(a, idx, mean, q, k), s);
+  return s;
+}
+
+__global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
+  __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[TMAX], s_map[KMAX + 1];
+  __shared__ double s_pot[TMAX], s_tol, s_red[NT];
+  __shared__ int s_ired[NT];
+  const int tid = threadIdx.x;
+  char* base = a.ws + static_cast<size_t>(blockIdx.x) * a.per_wg;
+  WG w;
+  w.mean = reinterpret_cast<double*>(base + a.o_mean);
+  w.xsq = reinterpret_cast<double*>(base + a.o_xsq);
+  w.cl = reinterpret_cast<double*>(base + a.o_cl);
+  w.dc = reinterpret_cast<double*>(base + a.o_dc);
+  w.sq = reinterpret_cast<double*>(base + a.o_sq);
+  w.cen = reinterpret_cast<double*>(base + a.o_cen);
+  w.cnew = reinterpret_cast<double*>(base + a.o_cnew);
+  w.lab = reinterpret_cast<int32_t*>(base + a.o_lab);
+  w.lold = reinterpret_cast<int32_t*>(base + a.o_lold);
+  w.lbest = reinterpret_cast<uint8_t*>(base + a.o_lbest);
+  const int m = a.m, d = a.d;
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) s_unit = static_cast<int>(atomicAdd(a.counter, 1u));
+    __syncthreads();
+    const int unit = s_unit;
+    if (unit >= a.nh * a.nK) break;
+    const int hb = unit / a.nK, kk = unit - hb * a.nK;
+    const int h = a.h_begin + hb;
+    const int K = a.Ks[kk];
+    const int ntr = 2 + static_cast<int>(log(static_cast<double>(K)));
+    const int32_t* idx = a.idx + static_cast<size_t>(h) * m;
+
+    // column means (rows in order), then variances of the centred columns
+    for (int k = tid; k < d; k += NT) {
+      double s = 0.0;
+      for (int r = 0; r < m; ++r) s += a.X[static_cast<size_t>(idx[r]) * d + k];
+      const double mu = s / m;
+      double q = 0.0;
+      for (int r = 0; r < m; ++r) {
+        const double t = a.X[static_cast<size_t>(idx[r]) * d + k] - mu;
+        q += t * t;
+      }
+      w.mean[k] = mu;
+      w.sq[k] = q / m;  // var (sq is free until the E-steps)
+    }
+    __syncthreads();
+    if (tid == 0) s_tol = (np_pairwise(w.sq, d) / d) * a.tol_rel;
+    // squared row norms of the centred rows
+    for (int r = tid; r < m; r += NT) {
+      double s = 0.0;
+      for (int k = 0; k < d; ++k) {
+        const double t = xc(a, idx, w.mean, r, k);
+        s += t * t;
+      }
+      w.xsq[r] = s;
+    }
+    __syncthreads();
+    const double tol = s_tol;
+
+    double best_inertia = 0.0;
+    int best_iter = 0;
+    for (int init = 0; init < a.n_init; ++init) {
+      const double* u = a.kpp_u + (static_cast<size_t>(kk) * a.n_init + init) * a.kpp_stride + 1;
+      // ---- k-means++ -------------------------------------------------------------
+      int cpos = a.kpp_pos[kk * a.n_init + init];
+      for (int k = tid; k < d; k += NT) w.cen[k] = xc(a, idx, w.mean, cpos, k);
+      for (int r = tid; r < m; r += NT) {
+        double dd = -2.0 * dotrr(a, idx, w.mean, cpos, r);
+        dd += w.xsq[cpos];
+        dd += w.xsq[r];
+        w.cl[r] = dd > 0.0 ? dd : 0.0;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        double pot = 0.0;
+        for (int r = 0; r < m; ++r) pot += w.cl[r];
+        s_pot[0] = pot;
+      }
+      __syncthreads();
+      double pot = s_pot[0];
+      for (int c = 1; c < K; ++c) {
+        // candidates: searchsorted(cumsum(closest), u * pot), clipped to m - 1
+        if (tid < ntr) {
+          const double rv = u[(c - 1) * ntr + tid] * pot;
+          double cum = 0.0;
+          int pos = m;
+          for (int r = 0; r < m; ++r) {
+            cum += w.cl[r];
+            if (!(cum < rv)) {
+              pos = r;
+              break;
+            }
+          }
+          s_cand[tid] = pos < m - 1 ? pos : m - 1;
+        }
+        __syncthreads();
+        for (int r = tid; r < m; r += NT) {
+          for (int t = 0; t < ntr; ++t) {
+            const int q = s_cand[t];
+            double dd = -2.0 * dotrr(a, idx, w.mean, q, r);
+            dd += w.xsq[q];
+            dd += w.xsq[r];
+            dd = dd > 0.0 ? dd : 0.0;
+            w.dc[static_cast<size_t>(t) * m + r] = w.cl[r] < dd ? w.cl[r] : dd;
+          }
+        }
+        __syncthreads();
+        if (tid < ntr) {
+          double s = 0.0;
+          for (int r = 0; r < m; ++r) s += w.dc[static_cast<size_t>(tid) * m + r];
+          s_pot[tid] = s;
+        }
+        __syncthreads();
+        int bt = 0;
+        for (int t = 1; t < ntr; ++t)
+          if (s_pot[t] < s_pot[bt]) bt = t;
+        pot = s_pot[bt];
+        cpos = s_cand[bt];
+        for (int r = tid; r < m; r += NT) w.cl[r] = w.dc[static_cast<size_t>(bt) * m + r];
+        for (int k = tid; k < d; k += NT) w.cen[static_cast<size_t>(c) * d + k] = xc(a, idx, w.mean, cpos, k);
+        __syncthreads();
+      }
+      // ---- Lloyd -------------------------------------------------------------------
+      for (int r = tid; r < m; r += NT) w.lold[r] = -1;
+      bool strict = false;
+      int it = 0;
+      double* cen = w.cen;
+      double* cnew = w.cnew;
+      for (it = 0; it < a.max_iter; ++it) {
+        // |c|^2 into s_red[0..K)
+        __syncthreads();
+        for (int j = tid; j < K; j += NT) {
+          double s = 0.0;
+          for (int k = 0; k < d; ++k) s += cen[static_cast<size_t>(j) * d + k] * cen[static_cast<size_t>(j) * d + k];
+          s_red[j] = s;
+        }
+        __syncthreads();
+        int chg = 0;
+        for (int r = tid; r < m; r += NT) {
+          double best = 0.0;
+          int lab = 0;
+          for (int j = 0; j < K; ++j) {
+            const double dj = __fma_rn(-2.0, dotc(a, idx, w.mean, r, cen + static_cast<size_t>(j) * d), s_red[j]);
+            if (j == 0 || dj < best) {
+              best = dj;
+              lab = j;
+            }
+          }
+          w.lab[r] = lab;
+          chg |= (lab != w.lold[r]);
+        }
+        const int changed = __syncthreads_or(chg);
+        // centre sums in row order: thread per feature
+        for (int k = tid; k < d; k += NT) {
+          for (int j = 0; j < K; ++j) cnew[static_cast<size_t>(j) * d + k] = 0.0;
+          for (int r = 0; r < m; ++r) cnew[static_cast<size_t>(w.lab[r]) * d + k] += xc(a, idx, w.mean, r, k);
+        }
+        if (tid == 0) {
+          for (int j = 0; j < K; ++j) s_ired[j] = 0;
+          for (int r = 0; r < m; ++r) s_ired[w.lab[r]] += 1;
+          int ne = 0;
+          for (int j = 0; j < K; ++j) ne += (s_ired[j] == 0);
+          s_flag = ne;
+        }
+        __syncthreads();
+        if (s_flag > 0) {
+          // _relocate_empty_clusters_dense: the empty clusters are fixed first (np.where), then
+          // each takes the farthest remaining row from its old centre (lowest index on ties)
+          for (int r = tid; r < m; r += NT) {
+            // ((X - centers_old[labels]) ** 2).sum(axis=1): numpy pairwise over the features
+            // (exact for d <= 128: one 8-accumulator block)
+            const double* c = cen + static_cast<size_t>(w.lab[r]) * d;
+            double s = 0.0;
+            if (d < 8) {
+              for (int k = 0; k < d; ++k) {
+                const double e = xc(a, idx, w.mean, r, k) - c[k];
+                s += e * e;
+              }
+            } else {
+              double v[8];
+              for (int q = 0; q < 8; ++q) {
+                const double e = xc(a, idx, w.mean, r, q) - c[q];
+                v[q] = e * e;
+              }
+              int k = 8;
+              for (; k < d - (d % 8); k += 8)
+                for (int q = 0; q < 8; ++q) {
+                  const double e = xc(a, idx, w.mean, r, k + q) - c[k + q];
+                  v[q] += e * e;
+                }
+              s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+              for (; k < d; ++k) {
+                const double e = xc(a, idx, w.mean, r, k) - c[k];
+                s += e * e;
+              }
+            }
+            w.sq[r] = s;
+          }
+          __syncthreads();
+          if (tid == 0) {
+            double mx = 0.0;
+            for (int r = 0; r < m; ++r) mx = w.sq[r] > mx ? w.sq[r] : mx;
+            int ne = 0;
+            for (int j = 0; j < K; ++j)
+              if (s_ired[j] == 0) s_map[ne++] = j;
+            s_flag = (mx == 0.0) ? 0 : ne;
+          }
+          __syncthreads();
+          const int ne = s_flag;
+          for (int e = 0; e < ne; ++e) {
+            if (tid == 0) {
+              int far = 0;
+              for (int r = 1; r < m; ++r)
+                if (w.sq[r] > w.sq[far]) far = r;
+              s_best[0] = far;
+            }
+            __syncthreads();
+            const int far = s_best[0], j = s_map[e], old = w.lab[far];
+            for (int k = tid; k < d; k += NT) {
+              const double x = xc(a, idx, w.mean, far, k);
+              cnew[static_cast<size_t>(old) * d + k] -= x;
+              cnew[static_cast<size_t>(j) * d + k] = x;
+            }
+            __syncthreads();
+            if (tid == 0) {
+              s_ired[j] = 1;
+              s_ired[old] -= 1;
+              w.sq[far] = -1.0;
+            }
+            __syncthreads();
+          }
+        }
+        // _average_centers: in cluster order; an empty cluster copies argmax(weight)'s row as it
+        // stands (still a raw sum when the argmax comes later)
+        if (tid == 0) {
+          int am = 0;
+          for (int j = 1; j < K; ++j)
+            if (s_ired[j] > s_ired[am]) am = j;
+          s_best[1] = am;
+        }
+        __syncthreads();
+        const int am = s_best[1];
+        for (int k = tid; k < d; k += NT)
+          for (int j = 0; j < K; ++j) {
+            double* cj = cnew + static_cast<size_t>(j) * d;
+            if (s_ired[j] > 0) cj[k] *= 1.0 / static_cast<double>(s_ired[j]);
+            else cj[k] = cnew[static_cast<size_t>(am) * d + k];
+          }
+        __syncthreads();
+        // shifts and convergence
+        if (tid < K) {
+          const double sh = sqrt(euclid4(cnew + static_cast<size_t>(tid) * d, cen + static_cast<size_t>(tid) * d, d));
+          s_red[NT - 1 - tid] = sh * sh;
+        }
+        __syncthreads();
+        double* tmp = cen;
+        cen = cnew;
+        cnew = tmp;
+        if (!changed) {
+          strict = true;
+          break;
+        }
+        double shifts[KMAX];
+        for (int j = 0; j < K; ++j) shifts[j] = s_red[NT - 1 - j];
+        const double tot = np_pairwise(shifts, K);
+        for (int r = tid; r < m; r += NT) w.lold[r] = w.lab[r];
+        if (tot <= tol) break;
+      }
+      const int n_iter = (it < a.max_iter ? it : a.max_iter - 1) + 1;
+      __syncthreads();
+      if (!strict) {  // final E-step against the last centres
+        for (int j = tid; j < K; j += NT) {
+          double s = 0.0;
+          for (int k = 0; k < d; ++k) s += cen[static_cast<size_t>(j) * d + k] * cen[static_cast<size_t>(j) * d + k];
+          s_red[j] = s;
+        }
+        __syncthreads();
+        for (int r = tid; r < m; r += NT) {
+          double best = 0.0;
+          int lab = 0;
+          for (int j = 0; j < K; ++j) {
+            const double dj = __fma_rn(-2.0, dotc(a, idx, w.mean, r, cen + static_cast<size_t>(j) * d), s_red[j]);
+            if (j == 0 || dj < best) {
+              best = dj;
+              lab = j;
+            }
+          }
+          w.lab[r] = lab;
+        }
+        __syncthreads();
+      }
+      // inertia: per-row squared distance to its centre, summed in row order
+      for (int r = tid; r < m; r += NT) {
+        const double* c = cen + static_cast<size_t>(w.lab[r]) * d;
+        double res = 0.0;
+        const int n4 = d / 4, rem = d % 4;
+        for (int i = 0; i < n4; ++i) {
+          const double d0 = xc(a, idx, w.mean, r, 4 * i) - c[4 * i];
+          const double d1 = xc(a, idx, w.mean, r, 4 * i + 1) - c[4 * i + 1];
+          const double d2 = xc(a, idx, w.mean, r, 4 * i + 2) - c[4 * i + 2];
+          const double d3 = xc(a, idx, w.mean, r, 4 * i + 3) - c[4 * i + 3];
+          res += ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;
+        }
+        for (int i = 0; i < rem; ++i) {
+          const double t = xc(a, idx, w.mean, r, 4 * n4 + i) - c[4 * n4 + i];
+          res += t * t;
+        }
+        w.sq[r] = res;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        double s = 0.0;
+        for (int r = 0; r < m; ++r) s += w.sq[r];
+        s_pot[0] = s;
+      }
+      __syncthreads();
+      const double inertia = s_pot[0];
+      // best of n_init: lower inertia AND a different clustering
+      bool take = (init == 0);
+      if (!take && inertia < best_inertia) {
+        for (int j = tid; j <= KMAX; j += NT) s_map[j] = -1;
+        __syncthreads();
+        if (tid == 0) {
+          int same = 1;
+          for (int r = 0; r < m && same; ++r) {
+            const int l1 = w.lab[r], l2 = w.lbest[r];
+            if (s_map[l1] == -1) s_map[l1] = l2;
+            else if (s_map[l1] != l2) same = 0;
+          }
+          s_flag = same;
+        }
+        __syncthreads();
+        take = !s_flag;
+      }
+      if (take) {
+        for (int r = tid; r < m; r += NT) w.lbest[r] = static_cast<uint8_t>(w.lab[r]);
+        best_inertia = inertia;
+        best_iter = n_iter;
+      }
+      __syncthreads();
+    }
+    uint8_t* out = a.labels + static_cast<size_t>(kk) * a.n * a.ldl + h;
+    for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = w.lbest[r];
+    if (tid == 0) {
+      if (a.inertia_out) a.inertia_out[static_cast<size_t>(kk) * a.H + h] = best_inertia;
+      if (a.niter_out) a.niter_out[static_cast<size_t>(kk) * a.H + h] = best_iter;
+    }
+  }
+}
+
+struct F64Layout {
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, per_wg;
+};
+
+F64Layout f64_layout(int m, int d, int kmax) {
+  auto al = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
+  F64Layout L{};
+  size_t o = 0;
+  L.o_mean = o;  o += al(sizeof(double) * std::max(d, 1));
+  L.o_xsq = o;   o += al(sizeof(double) * m);
+  L.o_cl = o;    o += al(sizeof(double) * m);
+  L.o_dc = o;    o += al(sizeof(double) * m * TMAX);
+  L.o_sq = o;    o += al(sizeof(double) * std::max(m, d));
+  L.o_cen = o;   o += al(sizeof(double) * kmax * d);
+  L.o_cnew = o;  o += al(sizeof(double) * kmax * d);
+  L.o_lab = o;   o += al(sizeof(int32_t) * m);
+  L.o_lold = o;  o += al(sizeof(int32_t) * m);
+  L.o_lbest = o; o += al(m);
+  L.per_wg = o;
+  return L;
+}
+
+constexpr size_t WS_HEADER = 256;
+
+}  // namespace
+
+extern "C" size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks, int nK, int grid) {
+  if (m <= 0 || d <= 0 || !Ks || nK <= 0 || grid <= 0) return 0;
+  int kmax = 1;
+  for (int i = 0; i < nK; ++i) kmax = std::max(kmax, Ks[i]);
+  return WS_HEADER + f64_layout(m, d, kmax).per_wg * static_cast<size_t>(grid);
+}
+
+extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_hm, int H, int m,
+                             int h_begin, int h_end, const int32_t* Ks, int nK, int n_init,
+                             int max_iter, double tol_rel, const double* kpp_u, int kpp_stride,
+                             const int32_t* kpp_pos, uint8_t* labels_nh, int ldl, double* inertia,
+                             int32_t* n_iter, void* workspace, size_t ws_bytes, int grid,
+                             void* stream) {
+  if (!X || !idx_hm || !Ks || !kpp_u || !kpp_pos || !labels_nh || n <= 0 || d <= 0 || m <= 0 ||
+      m > n || H <= 0 || h_begin < 0 || h_end > H || h_end < h_begin || nK <= 0 || nK > NKMAX ||
+      n_init <= 0 || max_iter <= 0 || ldl < H || grid <= 0) {
+    cc::set_error("cc_kmeans_f64: bad arguments");
+    return CC_ERR_ARG;
+  }
+  int kmax = 1, tmax = 0;
+  for (int i = 0; i < nK; ++i) {
+    if (Ks[i] < 1 || Ks[i] > KMAX || Ks[i] > m) {
+      cc::set_error("cc_kmeans_f64: need 1 <= K <= min(127, m)");
+      return CC_ERR_ARG;
+    }
+    kmax = std::max(kmax, Ks[i]);
+    tmax = std::max(tmax, 2 + static_cast<int>(std::log(static_cast<double>(Ks[i]))));
+  }
+  if (kpp_stride < 1 + (kmax - 1) * tmax) {
+    cc::set_error("cc_kmeans_f64: kpp_stride too small");
+    return CC_ERR_ARG;
+  }
+  const int nh = h_end - h_begin;
+  if (nh == 0) return CC_OK;
+  const F64Layout L = f64_layout(m, d, kmax);
+  if (!workspace || ws_bytes < WS_HEADER + L.per_wg * static_cast<size_t>(grid)) {
+    cc::set_error("cc_kmeans_f64: workspace too small");
+    return CC_ERR_ARG;
+  }
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(workspace, 0, sizeof(unsigned), st);
+  if (e != hipSuccess) {
+    cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));
+    return CC_ERR_HIP;
+  }
+  F64Args a{};
+  a.X = X;
+  a.n = n;
+  a.d = d;
+  a.idx = idx_hm;
+  a.H = H;
+  a.m = m;
+  a.h_begin = h_begin;
+  a.nh = nh;
+  a.nK = nK;
+  for (int i = 0; i < nK; ++i) a.Ks[i] = Ks[i];
+  a.n_init = n_init;
+  a.max_iter = max_iter;
+  a.tol_rel = tol_rel;
+  a.kpp_u = kpp_u;
+  a.kpp_stride = kpp_stride;
+  a.kpp_pos = kpp_pos;
+  a.labels = labels_nh;
+  a.ldl = ldl;
+  a.inertia_out = inertia;
+  a.niter_out = n_iter;
+  a.counter = static_cast<unsigned*>(workspace);
+  a.ws = static_cast<char*>(workspace) + WS_HEADER;
+  a.per_wg = L.per_wg;
+  a.o_mean = L.o_mean;
+  a.o_xsq = L.o_xsq;
+  a.o_cl = L.o_cl;
+  a.o_dc = L.o_dc;
+  a.o_sq = L.o_sq;
+  a.o_cen = L.o_cen;
+  a.o_cnew = L.o_cnew;
+  a.o_lab = L.o_lab;
+  a.o_lold = L.o_lold;
+  a.o_lbest = L.o_lbest;
+  const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nK));
+  hipLaunchKernelGGL(kmeans_f64_kernel, dim3(blocks), dim3(NT), 0, st, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) {
+    cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));
+    return CC_ERR_HIP;
+  }
+  return CC_OK;
+}

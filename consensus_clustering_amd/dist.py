@@ -15,10 +15,12 @@ independent and every count is an integer sum, so a fit shards exactly:
 * matrices    (only when requested) each rank's band of M / I, SUM all-reduce.
 
 Bit-exact for every W: integer counts, order-free reductions.
+
+The exchanges use the default process group.  With the ``gloo`` backend (CPU tests, and
+the single-GPU multi-process tests that put several ranks on one device) device tensors
+are reduced through a host copy; with ``nccl`` (RCCL) they are reduced in place.
 """
 from __future__ import annotations
-
-import os
 
 import torch
 import torch.distributed as dist
@@ -29,17 +31,9 @@ def _live() -> bool:
 
 
 def world() -> tuple:
-    """(rank, world_size) of the default process group, (0, 1) when not initialised.
-
-    ``CCMI_SIM_RANK=r/W`` (no process group) runs rank r's shard of a W-rank fit alone, with
-    the exchanges skipped: a one-GPU rehearsal of the per-rank critical path (timing only,
-    the results are partial)."""
+    """(rank, world_size) of the default process group, (0, 1) when not initialised."""
     if _live():
         return dist.get_rank(), dist.get_world_size()
-    sim = os.environ.get("CCMI_SIM_RANK")
-    if sim:
-        r, w = (int(v) for v in sim.split("/"))
-        return r, w
     return 0, 1
 
 
@@ -50,17 +44,25 @@ def shard(total: int, rank: int, world_size: int) -> tuple:
     return begin, begin + base + (1 if rank < rem else 0)
 
 
+def _all_reduce(t: torch.Tensor, op) -> torch.Tensor:
+    if not (_live() and dist.get_world_size() > 1):
+        return t
+    if t.is_cuda and dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
+
+
 def merge_labels(labels: torch.Tensor) -> torch.Tensor:
     """Assemble per-rank label matrices (0xFF where not owned) in place."""
-    if _live() and dist.get_world_size() > 1:
-        dist.all_reduce(labels, op=dist.ReduceOp.MIN)
-    return labels
+    return _all_reduce(labels, dist.ReduceOp.MIN)
 
 
 def sum_counts(t: torch.Tensor) -> torch.Tensor:
-    if _live() and dist.get_world_size() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return t
+    return _all_reduce(t, dist.ReduceOp.SUM)
 
 
 def barrier():

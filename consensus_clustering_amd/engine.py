@@ -172,3 +172,12 @@ def consensus(M: torch.Tensor, I: torch.Tensor) -> torch.Tensor:
     C = torch.empty((n, n), dtype=torch.float32, device=M.device)
     _lib.call("cc_consensus", M.data_ptr(), I.data_ptr(), n, C.data_ptr(), stream_ptr())
     return C
+
+
+def manhattan(C: torch.Tensor) -> torch.Tensor:
+    """float64 [n, n] manhattan distances between the rows of the float32 [n, n] C."""
+    assert C.dtype == torch.float32 and C.dim() == 2 and C.is_contiguous()
+    n, d = C.shape
+    D = torch.empty((n, n), dtype=torch.float64, device=C.device)
+    _lib.call("cc_manhattan", C.data_ptr(), n, d, D.data_ptr(), stream_ptr())
+    return D

@@ -209,6 +209,40 @@ class BatchedKMeans:
                       engine.stream_ptr(dev))
         return labels_nh
 
+    def run_f64(self, X64, idx_d, n, H, m, h_begin, h_end, labels_nh, inertia=None, n_iter=None,
+                grid=None):
+        """float64 path (cc_kmeans_f64): X64 is the raw [n, d] float64 input on the device."""
+        dev = X64.device
+        if max(self.Ks) > m:
+            raise ValueError(f"n_samples={m} should be >= n_clusters={max(self.Ks)}.")
+        self.stats = torch.zeros(128, dtype=torch.int64, device=dev)
+        nh = h_end - h_begin
+        if nh <= 0:
+            return labels_nh
+        lib = _lib.load()
+        d = X64.shape[1]
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        for k0 in range(0, len(self.Ks), 64):  # cc_kmeans_f64 takes <= 64 K values per call
+            Ks = self.Ks[k0:k0 + 64]
+            Ks_np = np.ascontiguousarray(np.asarray(Ks, dtype=np.int32))
+            g = int(grid or min(4 * cus, nh * len(Ks)))
+            per = lambda gg: lib.cc_kmeans_f64_workspace_bytes(m, d, Ks_np.ctypes.data, len(Ks), gg)
+            while g > 1 and per(g) > self.workspace_budget:
+                g //= 2
+            ws = workspace(dev, per(g))
+            u, pos, stride = kpp_tables(Ks, self.n_init, self.seed, m, np.float64)
+            u_d = torch.from_numpy(u).to(dev)
+            pos_d = torch.from_numpy(pos).to(dev)
+            with engine.timed("cc_kmeans_f64"):
+                _lib.call("cc_kmeans_f64", X64.data_ptr(), n, d, idx_d.data_ptr(), H, m, h_begin,
+                          h_end, Ks_np.ctypes.data, len(Ks), self.n_init, self.max_iter, self.tol,
+                          u_d.data_ptr(), stride, pos_d.data_ptr(), labels_nh[k0].data_ptr(),
+                          labels_nh.stride(1),
+                          None if inertia is None else inertia[k0].data_ptr(),
+                          None if n_iter is None else n_iter[k0].data_ptr(), ws.data_ptr(),
+                          ws.numel(), g, engine.stream_ptr(dev))
+        return labels_nh
+
     def _run_wide(self, Xd, xnorm, dreal, idx_d, n, H, m, h_begin, h_end, labels_nh, weight_dtype,
                   inertia, n_iter, Xhl, scale_exp):
         """d > 128: cc_kmeans_wide over batches of resamples sized to the workspace budget,

@@ -44,6 +44,10 @@ extern "C" {
 
 const char* cc_version(void);
 const char* cc_last_error(void);
+/* SHA-256 prefix (16 hex digits) of the sources and flags this library was built from
+ * (the .hip, .cpp and .h files of csrc, include/ccmi.h and the csrc Makefile); the Python host
+ * refuses a library whose id does not match the sources next to it. */
+const char* cc_build_id(void);
 
 /* ---- host-side helpers (native, no device) ------------------------------ */
 
@@ -97,8 +101,21 @@ int cc_bin_table(int rows, const float* edges, uint16_t* table, void* stream);
 /* Largest table (rows) cc_coassoc can stage on chip. */
 int cc_bin_table_max_rows(void);
 
+/* Self-test of the division-free binning: for EVERY pair of counts (m <= i < rows), compare
+ * the two table forms cc_coassoc uses (threshold table + reciprocal estimate computed per
+ * element, and with the staged per-row reciprocal) against the direct numpy-exact bin of
+ * f32(m) / f32(i + 1e-6).  mismatches: device [2] uint64, accumulated into. */
+int cc_bin_selftest(int rows, const float* edges, const uint16_t* table,
+                    unsigned long long* mismatches, void* stream);
+
 /* C = f32(M) / f32(f64(I) + 1e-6) with C_ii = 1 (CC.py:372-373), [n][n]. */
 int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stream);
+
+/* Manhattan distances between the rows of C [n][d] float32: D [n][n] float64,
+ * D_ij = sum_k |f64(C_ik) - f64(C_jk)| summed sequentially over k (scipy pdist 'cityblock'
+ * order), for the consensus labels of CC.py:292-314 (AgglomerativeClustering on the rows of C
+ * under the manhattan metric). */
+int cc_manhattan(const float* C, int n, int d, double* D, void* stream);
 
 /* Batched k-means for every (resample h, K, init) problem, replacing the per-(K, h)
  * clusterer.fit_predict(X[indices]) of CC.py:282 for the default clusterer
@@ -173,6 +190,21 @@ int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* xnorm, int 
                    uint8_t* labels_nh, int ldl, float* inertia, int32_t* n_iter,
                    unsigned long long* stats, void* workspace, size_t ws_bytes, int batch,
                    void* stream);
+
+/* Float64 k-means for float64 input (the reference's clusterer at the reference's precision,
+ * CC.py:282 with float64 X; sklearn/cluster/_kmeans.py restated in float64, see
+ * csrc/kmeans_f64.hip).  Same fits, outputs and k-means++ tables as cc_kmeans_batched; X is
+ * the raw [n][d] float64 input (the kernel centres each resample by its own mean, as
+ * KMeans.fit does).  Ks [nK] is a host array (nK <= 64); one persistent workgroup per
+ * (resample, K) unit; inertia is float64 here.  Workspace from
+ * cc_kmeans_f64_workspace_bytes(m, d, Ks, nK, grid). */
+size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks, int nK, int grid);
+
+int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_hm, int H, int m, int h_begin,
+                  int h_end, const int32_t* Ks, int nK, int n_init, int max_iter, double tol_rel,
+                  const double* kpp_u, int kpp_stride, const int32_t* kpp_pos, uint8_t* labels_nh,
+                  int ldl, double* inertia, int32_t* n_iter, void* workspace, size_t ws_bytes,
+                  int grid, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,65 @@
+"""Helper for tests/test_gpu_dist.py (not collected by pytest): runs ConsensusClustering.fit
+as a W-rank torch.distributed job (gloo backend, every rank on cuda:0) and saves rank 0's
+results.  It is started as a child process, so the ranks are spawned by a parent that has not
+touched the GPU.
+
+    python tests/dist_worker.py <fixture> <world> <keep 0|1> <out.npz>
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, name, keep, out):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from consensus_clustering_amd import ConsensusClustering
+        from tests.conftest import load_fixture
+
+        f = load_fixture(name)
+        meta = f["meta"]
+        cc = ConsensusClustering(K_range=[int(k) for k in f["K_range"]], n_iterations=meta["H"],
+                                 subsampling=meta["subsampling"], random_state=meta["random_state"],
+                                 plot_cdf=False, keep_matrices=bool(keep))
+        cc.fit(f["X"])
+        Ks = list(cc.cdf_at_K_data)
+        res = dict(
+            pair_counts=np.stack([cc.pair_counts_[K] for K in Ks]),
+            labels=cc.labels_.cpu().numpy(),
+            pac=np.array([cc.cdf_at_K_data[K]["pac_area"] for K in Ks]),
+            hist=np.stack([cc.cdf_at_K_data[K]["hist"] for K in Ks]),
+        )
+        if keep:
+            res["mij"] = np.stack([cc.cdf_at_K_data[K]["mij"] for K in Ks])
+            res["iij"] = cc.cdf_at_K_data[Ks[0]]["iij"]
+        if rank == 0:
+            np.savez(out, **res)
+    finally:
+        dist.destroy_process_group()
+
+
+def main():
+    import torch.multiprocessing as mp
+
+    name, world, keep, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    mp.spawn(_rank, args=(world, _free_port(), name, keep, out), nprocs=world, join=True)
+
+
+if __name__ == "__main__":
+    main()

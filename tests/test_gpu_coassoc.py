@@ -155,3 +155,19 @@ def test_threshold_table_binning_is_exact(H, K):
         ref = np.clip(np.searchsorted(e32, x, side="right") - 1, 0, 19)
         got = (m[:, None] >= tab[i, 1:20][None, :]).sum(axis=1)
         np.testing.assert_array_equal(got, ref, err_msg=f"i={i}")
+
+
+def test_bin_table_exhaustive():
+    """Every (m <= i) pair of counts the on-chip table can hold (i < cc_bin_table_max_rows(),
+    i.e. H up to ~1940): both division-free forms give the numpy-exact bin of
+    f32(m) / f32(i + 1e-6) (CC.py:338-344, :372)."""
+    from consensus_clustering_amd import _lib
+
+    dev = engine.require_gpu()
+    rows = _lib.load().cc_bin_table_max_rows()
+    tab = engine.bin_table(dev, rows)
+    mism = torch.zeros(2, dtype=torch.int64, device=dev)
+    _lib.call("cc_bin_selftest", rows, engine.edges_device(dev).data_ptr(), tab.data_ptr(),
+              mism.data_ptr(), engine.stream_ptr())
+    torch.cuda.synchronize()
+    assert mism.tolist() == [0, 0], (rows, mism.tolist())

@@ -193,3 +193,40 @@ def test_wide_expression_like():
                 total += 1
     assert agree >= 0.7 * total, f"{agree}/{total}"
     assert np.all(np.isfinite(inert))
+
+
+@pytest.mark.parametrize("n,d,k_true,Ks,H", [
+    (29, 29, 3, [2, 3, 4, 5, 6, 7, 8, 9, 10], 6),
+    (600, 12, 4, [2, 3, 4, 6, 9], 4),
+    (300, 150, 3, [2, 3, 5], 3),
+])
+def test_f64_labels_match_sklearn_float64(n, d, k_true, Ks, H):
+    """float64 input, float64 path (cc_kmeans_f64): sklearn's own float64 KMeans on the same
+    resamples, every K — including K above the true blob count, where only an identical
+    arithmetic class reproduces sklearn's partitions."""
+    from threadpoolctl import threadpool_limits
+
+    seed = 3
+    X = blobs(n, d, k_true, seed=n + d).astype(np.float64)
+    X += np.random.default_rng(0).normal(scale=0.5, size=X.shape)  # break exact symmetry
+    dev = engine.require_gpu()
+    m = int(0.8 * n)
+    idx = engine.resample_indices(seed, n, m, 0, H)
+    idx_d = torch.from_numpy(idx).to(dev)
+    L = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
+    inert = torch.zeros((len(Ks), H), dtype=torch.float64, device=dev)
+    nit = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
+    BatchedKMeans(Ks, n_init=3, random_state=seed).run_f64(
+        torch.from_numpy(X).to(dev), idx_d, n, H, m, 0, H, L, inertia=inert, n_iter=nit)
+    torch.cuda.synchronize()
+    Lh = L.cpu().numpy()
+    with threadpool_limits(1):
+        for k, K in enumerate(Ks):
+            for h in range(H):
+                from sklearn.cluster import KMeans
+
+                km = KMeans(n_clusters=K, random_state=seed, n_init=3).fit(X[idx[h]])
+                got = Lh[k][idx[h], h].astype(np.int64)
+                assert np.array_equal(km.labels_, got), (K, h, np.mean(km.labels_ == got))
+                assert nit[k, h].item() == km.n_iter_, (K, h)
+                np.testing.assert_allclose(inert[k, h].item(), km.inertia_, rtol=1e-12)

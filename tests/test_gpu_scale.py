@@ -1,0 +1,200 @@
+"""BASELINE configs 2, 3 and 5 at their full size: the fits the bench times, checked for
+correctness (VERDICT r1 "configs_untested").
+
+For each config the drop-in fit runs at the real n, d, K range and H, then:
+  * every K's strict-upper pair counts sum to n(n-1)/2 (CC.py:338, every pair binned once);
+  * every resample column of the label matrix holds exactly its m sampled rows (the rows of
+    RandomState(seed + h).permutation(n)[:m], CC.py:216-241), each with a label in [0, K);
+  * a set of 256 x 256 tiles spread over the triangle (first, middle, last row bands; the
+    ragged last column block; diagonal tiles) is recomputed on the host from the fit's own
+    labels: the co-sampling tile (diagonal = per-row sample counts) and the 20 histogram
+    counts of every K must be bit-identical to the GPU's (CC.py:264, :287-290, :338-344);
+  * C2 / C3: the k-means labels of the first resamples at the full m equal sklearn's
+    KMeans (the reference's clusterer, CC.py:282) for every K <= the true number of blobs.
+C2 (n = 10k) also keeps the full matrices: iij and mij are compared with the oracle's.
+"""
+import numpy as np
+import pytest
+import torch
+
+from bench import CONFIGS, SEED, make_blobs_f32
+from consensus_clustering_amd import engine, post
+from oracle import cc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TILE = 256
+
+
+def tile_start(b, nb):
+    return b * nb - b * (b - 1) // 2
+
+
+def tile_index(bi, bj, nb):
+    return tile_start(bi, nb) + (bj - bi)
+
+
+def decode_I_tile(raw):
+    """uint16 co-sampling tile in cc_cosample's accumulator order -> [256, 256] (row, col)."""
+    v = raw.astype(np.int64) & 0xFFFF
+    out = np.zeros((TILE, TILE), dtype=np.int64)
+    tid = np.arange(512)
+    wave, lane = tid >> 6, tid & 63
+    wr, wc = wave >> 2, wave & 3
+    e = 0
+    vals = v.reshape(512, 128)
+    for mi in range(4):
+        for nj in range(2):
+            for r in range(16):
+                row = wr * 128 + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+                col = wc * 64 + nj * 32 + (lane & 31)
+                out[row, col] = vals[:, e]
+                e += 1
+    return out
+
+
+def host_tile(Lk, bi, bj, n):
+    """I and M of tile (bi, bj) from the host copy of one K's label rows (uint8, 0xFF = not
+    sampled): I_ij = #h both sampled, M_ij = #h same label."""
+    ri = np.arange(bi * TILE, min(n, (bi + 1) * TILE))
+    rj = np.arange(bj * TILE, min(n, (bj + 1) * TILE))
+    A, B = Lk[ri], Lk[rj]                     # [rows, H]
+    sa, sb = A != 0xFF, B != 0xFF
+    I = sa.astype(np.float32) @ sb.T.astype(np.float32)
+    M = np.zeros((len(ri), len(rj)), dtype=np.float32)
+    for c in range(int(A[sa].max(initial=0)) + 1):
+        M += (A == c).astype(np.float32) @ (B == c).T.astype(np.float32)
+    return ri, rj, np.rint(I).astype(np.int64), np.rint(M).astype(np.int64)
+
+
+def tile_pair_counts(ri, rj, I, M):
+    """numpy.histogram counts of C = M / (I + 1e-6) (CC.py:372) over the tile's strict-upper
+    pairs i < j."""
+    C = np.divide(M.astype(np.uint16), I.astype(np.uint16) + 1e-6, dtype=np.float32)
+    mask = ri[:, None] < rj[None, :]
+    return np.histogram(C[mask], bins=20, range=(0, 1))[0].astype(np.int64)
+
+
+def fit_config(name, keep=False):
+    from consensus_clustering_amd import ConsensusClustering
+
+    cfg = CONFIGS[name]
+    X = make_blobs_f32(cfg["n"], cfg["d"], cfg["k_true"], seed=SEED)
+    cc = ConsensusClustering(K_range=cfg["Ks"], n_iterations=cfg["H"], subsampling=cfg["frac"],
+                             random_state=SEED, plot_cdf=False, keep_matrices=keep)
+    cc.fit(torch.from_numpy(X).to(engine.require_gpu()))
+    torch.cuda.synchronize()
+    return cfg, X, cc
+
+
+def check_labels(cfg, cc):
+    n, H = cfg["n"], cfg["H"]
+    m = int(cfg["frac"] * n)
+    L = cc.labels_
+    idx = torch.from_numpy(cc.resampling_indices_.astype(np.int64)).to(L.device)
+    want = torch.zeros((n, L.shape[2]), dtype=torch.bool, device=L.device)
+    want[idx, torch.arange(H, device=L.device)[:, None].expand(H, m)] = True
+    for k, K in enumerate(cfg["Ks"]):
+        samp = L[k] != 0xFF
+        assert torch.equal(samp, want), f"K={K}: sampled set differs"
+        assert int((L[k][samp] >= K).sum()) == 0, f"K={K}: label out of range"
+        assert int(samp.sum(dim=0)[:H].min()) == m and int(samp.sum(dim=0)[:H].max()) == m
+
+
+def check_counts_sum(cfg, cc):
+    n = cfg["n"]
+    for K in cfg["Ks"]:
+        assert int(cc.pair_counts_[K].sum()) == n * (n - 1) // 2, K
+        hist, cdf, edges, pac = post.cdf_from_counts(
+            post.pair_counts_to_hist_counts(cc.pair_counts_[K], n))
+        np.testing.assert_array_equal(hist, cc.cdf_at_K_data[K]["hist"])
+
+
+def check_tiles(cfg, cc, Ks_check=None):
+    n = cfg["n"]
+    nb = (n + TILE - 1) // TILE
+    Ks = cfg["Ks"]
+    Ks_check = Ks_check or Ks
+    mid = nb // 2
+    picks = sorted({(0, 0), (0, 1), (0, nb - 1), (mid, mid), (mid, mid + 1 if mid + 1 < nb else mid),
+                    (mid, nb - 1), (nb - 1, nb - 1), (nb - 2, nb - 1)})
+    L = cc.labels_
+    Hpad = L.shape[2]
+    dev = L.device
+    edges = engine.edges_device(dev)
+    for (bi, bj) in picks:
+        t = tile_index(bi, bj, nb)
+        I_tiles, _ = engine.cosample(L[0], n, Hpad, t, t + 1)
+        rows = np.unique(np.r_[np.arange(bi * TILE, min(n, (bi + 1) * TILE)),
+                               np.arange(bj * TILE, min(n, (bj + 1) * TILE))])
+        Iraw = I_tiles.cpu().numpy().view(np.uint16)[0]
+        Ig = decode_I_tile(Iraw)
+        for k, K in enumerate(Ks):
+            if K not in Ks_check and k != 0:
+                continue
+            Lk = np.full((n, Hpad), 0xFF, dtype=np.uint8)
+            Lk[rows] = L[k][torch.from_numpy(rows).to(dev)].cpu().numpy()
+            ri, rj, I, M = host_tile(Lk, bi, bj, n)
+            if k == 0:  # the co-sampling tile itself, including the diagonal of diagonal tiles
+                np.testing.assert_array_equal(Ig[: len(ri), : len(rj)], I, err_msg=f"I tile {(bi, bj)}")
+                if bi == bj:
+                    np.testing.assert_array_equal(np.diag(I), (Lk[ri] != 0xFF).sum(axis=1))
+            if K not in Ks_check:
+                continue
+            counts = torch.zeros(20, dtype=torch.int64, device=dev)
+            engine.coassoc(L[k], n, Hpad, K, t, t + 1, I_tiles, edges, counts)
+            np.testing.assert_array_equal(counts.cpu().numpy(), tile_pair_counts(ri, rj, I, M),
+                                          err_msg=f"tile {(bi, bj)} K={K}")
+
+
+def check_kmeans(cfg, X, cc, resamples):
+    from threadpoolctl import threadpool_limits
+
+    L = cc.labels_
+    idx = cc.resampling_indices_
+    with threadpool_limits(16):
+        for k, K in enumerate(cfg["Ks"]):
+            if K > cfg["k_true"]:
+                continue
+            col = L[k].cpu().numpy()
+            for h in range(resamples):
+                ref = O.kmeans_labels(X[idx[h]], K, SEED, n_init=3)
+                got = col[idx[h], h].astype(np.int64)
+                assert np.array_equal(ref, got), (K, h, float(np.mean(ref == got)))
+
+
+def test_c3_full_size():
+    cfg, X, cc = fit_config("c3")
+    check_counts_sum(cfg, cc)
+    check_labels(cfg, cc)
+    check_tiles(cfg, cc, Ks_check=[2, 8, 13, 20])
+    check_kmeans(cfg, X, cc, resamples=2)
+
+
+def test_c5_full_size():
+    cfg, X, cc = fit_config("c5")
+    check_counts_sum(cfg, cc)
+    check_labels(cfg, cc)
+    check_tiles(cfg, cc, Ks_check=[2, 6, 10])
+
+
+def test_c2_full_size_with_matrices():
+    cfg, X, cc = fit_config("c2", keep=True)
+    check_counts_sum(cfg, cc)
+    check_labels(cfg, cc)
+    check_kmeans(cfg, X, cc, resamples=3)
+    n = cfg["n"]
+    idx = cc.resampling_indices_.astype(np.int64)
+    I_ref = O.cosample_matrix(idx, n)
+    np.testing.assert_array_equal(cc.cdf_at_K_data[cfg["Ks"][0]]["iij"], I_ref.astype(np.uint16))
+    L = cc.labels_
+    for K in (2, 6, 15):
+        k = cfg["Ks"].index(K)
+        col = L[k].cpu().numpy()
+        labs = np.stack([col[idx[h], h] for h in range(cfg["H"])]).astype(np.int64)
+        M_ref = O.coassoc_matrix(idx, labs, K, n)
+        np.testing.assert_array_equal(cc.cdf_at_K_data[K]["mij"], M_ref.astype(np.uint16))
+        ref = O.analyse(M_ref, I_ref, dtype=np.uint16)
+        for key in ("hist", "cdf", "bin_edges"):
+            np.testing.assert_array_equal(cc.cdf_at_K_data[K][key], ref[key])
+        assert cc.cdf_at_K_data[K]["pac_area"] == ref["pac_area"]
