@@ -586,6 +586,7 @@ extern "C" int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, in
                            int64_t tile_end, uint16_t* I_tiles, int32_t* I_full, void* stream) {
   int rc = check_common("cc_cosample", labels_nh, n, ldl, Hpad, tile_begin, tile_end);
   if (rc) return rc;
+  if (tile_end == tile_begin) return CC_OK;  // an empty band (a rank with no tiles)
   if (!I_tiles) {
     cc::set_error("cc_cosample: I_tiles is NULL");
     return CC_ERR_ARG;
@@ -637,6 +638,7 @@ extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int
     cc::set_error("cc_coassoc: K must be in [1, 127]");
     return CC_ERR_ARG;
   }
+  if (tile_end == tile_begin) return CC_OK;  // an empty band (a rank with no tiles)
   if (!I_tiles || !edges || !bin_counts) {
     cc::set_error("cc_coassoc: I_tiles, edges and bin_counts are required");
     return CC_ERR_ARG;
