@@ -1455,7 +1455,9 @@ struct Lay4 {
   static constexpr int SLOT = 2 * IMG;
   static constexpr int RING = NRING4 * SLOT;
   static constexpr int S_BYTES = CW * DP * 4;                 // centre sums [CW][DP] f32 (aliases the ring)
-  static constexpr int U_END = RING > S_BYTES ? RING : S_BYTES;
+  static constexpr int OFF_POT = RING;                         // seeding partials [NW][16][64] f32
+  static constexpr int POT_END = RING + NW * 16 * 64 * 4;
+  static constexpr int U_END = POT_END > S_BYTES ? POT_END : S_BYTES;
   static constexpr int OFF_LW = (U_END + 15) / 16 * 16;       // labels [NW][2][NCH][RT] u8
   static constexpr int OFF_XN = OFF_LW + NW * 2 * NCH * RT;   // row norms [NRING4][64] f32
   static constexpr int OFF_ST = OFF_XN + NRING4 * 64 * 4;
@@ -1600,87 +1602,79 @@ struct Wave4 {
 // potential partials of the columns).
 template <int DP>
 __device__ __forceinline__ void estep4(const KArgs& a, const Wave4& W, int te, int lane, const v16f& acc,
-                                       const float (&cn)[16], float xn, uint8_t* lw, float* dbuf, int T1,
-                                       const float (&pre)[4], float (&iacc)[NCH], float (&pot)[16]) {
+                                       const float* cnw, float xn, uint8_t* lw, float* dbuf, int T1,
+                                       const float (&pre)[4], float (&iacc)[NCH], float* pot) {
   const int r = lane & 31, hh = lane >> 5;
   const int erow = te * RT + r;
   const bool eok = erow < a.m;
-  float d[16];
+  float bm = 0.f;  // running (min, slot) of the Lloyd problem being merged, in chunk order
+  int bi = 0;
+  // One register group (4 distances, this lane's chunk 2g + hh) at a time: its chunk argmin is
+  // swapped with the other half's, then chunks 2g and 2g + 1 enter the merge in slot order.
 #pragma unroll
-  for (int v = 0; v < 16; ++v) d[v] = cn[v] - a.dscale * acc[v];
-  if (W.lin) {
-    float mg[4];
-    int ig[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {  // first argmin of this lane's chunk 2g + hh (strict <)
-      float m = d[4 * g];
+  for (int g = 0; g < 4; ++g) {
+    const unsigned gl = (W.lin >> (2 * g)) & 3u, gs = (W.smask >> (2 * g)) & 3u;
+    if ((gl | gs) == 0) continue;  // wave-uniform
+    float d[4];
+    {
+      const float4 c4 = *reinterpret_cast<const float4*>(cnw + 8 * g + 4 * hh);
+      d[0] = c4.x - a.dscale * acc[4 * g];
+      d[1] = c4.y - a.dscale * acc[4 * g + 1];
+      d[2] = c4.z - a.dscale * acc[4 * g + 2];
+      d[3] = c4.w - a.dscale * acc[4 * g + 3];
+    }
+    if (gl) {
+      float m = d[0];
       int j = 0;
 #pragma unroll
       for (int q = 1; q < 4; ++q)
-        if (d[4 * g + q] < m) {
-          m = d[4 * g + q];
+        if (d[q] < m) {
+          m = d[q];
           j = q;
         }
-      mg[g] = m;
-      ig[g] = 8 * g + 4 * hh + j;
-    }
-    float mc[NCH];
-    int ic[NCH];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if (((W.lin >> (2 * g)) & 3u) == 0) {
-        mc[2 * g] = mc[2 * g + 1] = 0.f;
-        ic[2 * g] = ic[2 * g + 1] = 0;
-        continue;
-      }
-      const auto bs = __builtin_amdgcn_permlane32_swap(__float_as_uint(mg[g]), __float_as_uint(mg[g]), false, false);
-      const auto is = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(ig[g]), static_cast<unsigned>(ig[g]), false, false);
+      const int i = 8 * g + 4 * hh + j;
+      const auto bs = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+      const auto is = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(i), static_cast<unsigned>(i), false, false);
       const float om = __uint_as_float(hh ? bs[0] : bs[1]);
       const int oi = static_cast<int>(hh ? is[0] : is[1]);
-      mc[2 * g] = hh ? om : mg[g];
-      ic[2 * g] = hh ? oi : ig[g];
-      mc[2 * g + 1] = hh ? mg[g] : om;
-      ic[2 * g + 1] = hh ? ig[g] : oi;
-    }
-    float bm = 0.f;
-    int bi = 0;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      if (!((W.lin >> c) & 1u)) continue;
-      if ((W.lstart >> c) & 1u) {
-        bm = mc[c];
-        bi = ic[c];
-      } else if (mc[c] < bm) {
-        bm = mc[c];
-        bi = ic[c];
-      }
-      if ((W.lend >> c) & 1u) {
-        const int lab = bi - static_cast<int>((W.cw[c] >> 8) & 0xFFu);
-        if (hh == 0) {
-          lw[c * RT + r] = eok ? static_cast<uint8_t>(lab) : static_cast<uint8_t>(0xFF);
-          if (eok) iacc[c] += xn + bm;
+      for (int e = 0; e < 2; ++e) {  // chunk 2g (half 0's), then 2g + 1 (half 1's)
+        const int c = 2 * g + e;
+        if (!((W.lin >> c) & 1u)) continue;
+        const float mc = (hh == e) ? m : om;
+        const int ic = (hh == e) ? i : oi;
+        if ((W.lstart >> c) & 1u) {
+          bm = mc;
+          bi = ic;
+        } else if (mc < bm) {
+          bm = mc;
+          bi = ic;
+        }
+        if ((W.lend >> c) & 1u) {
+          const int lab = bi - static_cast<int>((W.cw[c] >> 8) & 0xFFu);
+          if (hh == 0) {
+            lw[c * RT + r] = eok ? static_cast<uint8_t>(lab) : static_cast<uint8_t>(0xFF);
+            if (eok) iacc[c] += xn + bm;
+          }
         }
       }
     }
-  }
-  if (W.smask) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if (((W.smask >> (2 * g)) & 3u) == 0) continue;
+    if (gs) {
       const bool mine = (W.smask >> (2 * g + hh)) & 1u;
-      const unsigned w = hh ? W.cw[2 * g + 1] : W.cw[2 * g];
+      unsigned w = hh ? W.cw[2 * g + 1] : W.cw[2 * g];
+      asm volatile("" : "+v"(w));  // recompute the column addresses per tile rather than hold 16
       if (mine && eok) {
         const int sslot = w & 31, cs = (w >> 5) & 7, t0 = (w >> 8) & 7, ncol = (w >> 11) & 7;
         const bool seed = (w >> 14) & 1u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (j >= ncol) break;
-          const float dist = fmaxf(xn + d[4 * g + j], 0.f);
+          const float dist = fmaxf(xn + d[j], 0.f);
           const float dm = seed ? fminf(pre[g], dist) : dist;
           const int t = t0 + j;
           const int ws = seed ? ((t < cs) ? t : t + 1) : 0;
           dbuf[(static_cast<size_t>(sslot) * T1 + ws) * a.lsm + erow] = dm;
-          pot[4 * g + j] += dm;
+          pot[(4 * g + j) * 64] += dm;
         }
       }
     }
@@ -1698,7 +1692,8 @@ __device__ __forceinline__ void prefetch4(const KArgs& a, const Wave4& W, int tp
     pre[g] = 0.f;
     if (((W.smask >> (2 * g)) & 3u) == 0) continue;
     const bool mine = (W.smask >> (2 * g + hh)) & 1u;
-    const unsigned w = hh ? W.cw[2 * g + 1] : W.cw[2 * g];
+    unsigned w = hh ? W.cw[2 * g + 1] : W.cw[2 * g];
+    asm volatile("" : "+v"(w));
     if (mine && ok && ((w >> 14) & 1u))
       pre[g] = dbuf[(static_cast<size_t>(w & 31) * T1 + ((w >> 5) & 7)) * a.lsm + row];
   }
@@ -1706,7 +1701,7 @@ __device__ __forceinline__ void prefetch4(const KArgs& a, const Wave4& W, int tp
 
 // Add the f32 partials into the items' f64 accumulators (one contributing half per item: half 0
 // for Lloyd problems, the chunk's half for seeding columns) and restart them.
-__device__ __forceinline__ void flush4(State4& S, const Wave4& W, int lane, float (&iacc)[NCH], float (&pot)[16]) {
+__device__ __forceinline__ void flush4(State4& S, const Wave4& W, int lane, float (&iacc)[NCH], float* pot) {
   const int r = lane & 31, hh = lane >> 5;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -1723,9 +1718,9 @@ __device__ __forceinline__ void flush4(State4& S, const Wave4& W, int lane, floa
     const int ncol = (w >> 11) & 7, item0 = (w >> 16) & 0xFF;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const double v = half_sum(static_cast<double>(pot[4 * g + j]));
+      const double v = half_sum(static_cast<double>(pot[(4 * g + j) * 64]));
       if (mine && r == 0 && j < ncol) S.iinert[item0 + j] += v;
-      pot[4 * g + j] = 0.f;
+      pot[(4 * g + j) * 64] = 0.f;
     }
   }
 }
@@ -1868,11 +1863,12 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
       const int lp = static_cast<int>(S.cword[wave][lcq] & 0x3Fu);
       uint8_t* lgl = glab + static_cast<size_t>(lst ? lp : 0) * a.lsm + lrq;
       bool chg = false;
-      float iacc[NCH], pot[16];
+      float iacc[NCH];
 #pragma unroll
       for (int c = 0; c < NCH; ++c) iacc[c] = 0.f;
+      float* pot = reinterpret_cast<float*>(smem + LY::OFF_POT) + wave * (16 * 64) + lane;
 #pragma unroll
-      for (int v = 0; v < 16; ++v) pot[v] = 0.f;
+      for (int v = 0; v < 16; ++v) pot[v * 64] = 0.f;
       // pipeline prologue: tile 0 in the ring, indices of tile 1; operands of tile 0
       TileIdx<DP> nI;
       {
@@ -1886,16 +1882,12 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
       prefetch4(a, W, 0, lane, dbuf, T1, pre);
       unsigned lold = lst ? *reinterpret_cast<const unsigned*>(lgl) : 0u;
       __syncthreads();  // cnorm, iinert, tile 0
-      float cn[16];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 c4 = *reinterpret_cast<const float4*>(S.cnorm + 32 * wave + 8 * g4 + 4 * hh);
-        cn[4 * g4] = c4.x;
-        cn[4 * g4 + 1] = c4.y;
-        cn[4 * g4 + 2] = c4.z;
-        cn[4 * g4 + 3] = c4.w;
-      }
+      const float* cnw = S.cnorm + 32 * wave;
+#ifdef CC_KM_STAMPS
+      unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
       for (int t = 0; t < T; ++t) {
+        KM_STAMP(s0);
         // gather: rows of tile t+1 by LDS-DMA (indices loaded last iteration), indices of t+2;
         // operands of tile t+1
         if (t + 1 < T) tile_dma<DP>(a, nI, ring + ((t + 1) % NRING4) * LY::SLOT, XN + ((t + 1) % NRING4) * 64, wave, lane);
@@ -1904,6 +1896,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
         prefetch4(a, W, t + 1, lane, dbuf, T1, npre);
         const unsigned nlold = (lst && t + 1 < T) ? *reinterpret_cast<const unsigned*>(lgl + (t + 1) * RT) : 0u;
         __builtin_amdgcn_sched_barrier(0);
+        KM_STAMP(s1);
         const char* xs = ring + (t % NRING4) * LY::SLOT;
         uint8_t* lw = lwave + (t & 1) * (NCH * RT);
         if (tact) {
@@ -1930,10 +1923,13 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
               bl = nl;
             }
           }
+          KM_STAMP(s2i);
+          KM_ACC(1, s1, s2i);
           const float xn = XN[(t % NRING4) * 64 + lr];
-          estep4<DP>(a, W, t, lane, acc, cn, xn, lw, dbuf, T1, pre, iacc, pot);
+          estep4<DP>(a, W, t, lane, acc, cnw, xn, lw, dbuf, T1, pre, iacc, pot);
         }
         __builtin_amdgcn_wave_barrier();
+        KM_STAMP(s3);
         // M-step of tile t (one-hot x X on f16 MFMA; counts by popcount)
         if (mact) {
           const uint8_t* lsb = lw + myend * RT;
@@ -1979,6 +1975,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
             }
           }
         }
+        KM_STAMP(s4);
         // labels of tile t: compare with the previous sweep's, store (one dword = 4 rows per lane)
         if (lst) {
           const unsigned w32 = *reinterpret_cast<const unsigned*>(lw + lcq * RT + lrq);
@@ -1990,8 +1987,19 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
         for (int i = 0; i < 4; ++i) pre[i] = npre[i];
         lold = nlold;
         dma_wait();
+        KM_STAMP(s5);
         __syncthreads();
+        KM_STAMP(s6);
+        KM_ACC(0, s0, s1);
+        KM_ACC(2, s1, s3);  // distances + E-step (the distance share is stamp 1 of active waves)
+        KM_ACC(3, s3, s4);
+        KM_ACC(4, s4, s5);
+        KM_ACC(5, s5, s6);
       }
+#ifdef CC_KM_STAMPS
+      if (blockIdx.x == 0 && lane == 0 && a.stats)
+        for (int k = 0; k < 7; ++k) atomicAdd(&a.stats[8 + 8 * wave + k], st_acc[k]);
+#endif
       flush4(S, W, lane, iacc, pot);
       // labels changed, per Lloyd problem of this wave
 #pragma unroll

@@ -10,6 +10,7 @@
 //   * k-means++ (_kmeans_plusplus): squared distances ((-2 x.c) + |c|^2) + |x|^2 clipped at 0
 //     (_euclidean_distances), candidates by searchsorted over the float64 cumsum, the
 //     candidate with the lowest potential kept;
+//   * squared norms of rows and centres in numpy einsum's order (row_norms);
 //   * Lloyd (_kmeans_single_lloyd / lloyd_iter_chunked_dense): distances |c|^2 - 2 x.c,
 //     argmin with strict < (lowest index on ties), centre sums in row order, empty clusters
 //     relocated to the farthest points, averaging with 1/weight, shifts by the 4-way unrolled
@@ -84,6 +85,28 @@ __device__ double np_pairwise(const double* a, int n) {
   int n2 = n / 2;
   n2 -= n2 % 8;
   return np_pairwise(a, n2) + np_pairwise(a + n2, n - n2);
+}
+
+// sklearn row_norms(X, squared=True) = np.einsum('ij,ij->i', X, X): numpy's contiguous
+// sum-of-products kernel (einsum_sumprod.c.src) on the x86-64 baseline: 2 double lanes, blocks
+// of 8 accumulated as lane += a0 b0 + (a1 b1 + (a2 b2 + (a3 b3 + lane)))) (separate multiply and
+// add), a zero-filled tail in lane steps, then lane 0 + lane 1.
+template <class F>
+__device__ __forceinline__ double einsum_sq(F x, int d) {
+  double l0 = 0.0, l1 = 0.0;
+  int i = 0;
+  for (; d - i >= 8; i += 8) {
+    const double a0 = x(i), a1 = x(i + 1), a2 = x(i + 2), a3 = x(i + 3);
+    const double a4 = x(i + 4), a5 = x(i + 5), a6 = x(i + 6), a7 = x(i + 7);
+    l0 = a0 * a0 + (a2 * a2 + (a4 * a4 + (a6 * a6 + l0)));
+    l1 = a1 * a1 + (a3 * a3 + (a5 * a5 + (a7 * a7 + l1)));
+  }
+  for (; i < d; i += 2) {
+    const double a = x(i), b = (i + 1 < d) ? x(i + 1) : 0.0;
+    l0 = a * a + l0;
+    l1 = b * b + l1;
+  }
+  return l0 + l1;
 }
 
 // _euclidean_dense_dense (squared): 4-way unrolled, left to right
@@ -171,14 +194,8 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
     __syncthreads();
     if (tid == 0) s_tol = (np_pairwise(w.sq, d) / d) * a.tol_rel;
     // squared row norms of the centred rows
-    for (int r = tid; r < m; r += NT) {
-      double s = 0.0;
-      for (int k = 0; k < d; ++k) {
-        const double t = xc(a, idx, w.mean, r, k);
-        s += t * t;
-      }
-      w.xsq[r] = s;
-    }
+    for (int r = tid; r < m; r += NT)
+      w.xsq[r] = einsum_sq([&](int k) { return xc(a, idx, w.mean, r, k); }, d);
     __syncthreads();
     const double tol = s_tol;
 
@@ -255,9 +272,8 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
         // |c|^2 into s_red[0..K)
         __syncthreads();
         for (int j = tid; j < K; j += NT) {
-          double s = 0.0;
-          for (int k = 0; k < d; ++k) s += cen[static_cast<size_t>(j) * d + k] * cen[static_cast<size_t>(j) * d + k];
-          s_red[j] = s;
+          const double* cj = cen + static_cast<size_t>(j) * d;
+          s_red[j] = einsum_sq([&](int k) { return cj[k]; }, d);
         }
         __syncthreads();
         int chg = 0;
@@ -395,9 +411,8 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
       __syncthreads();
       if (!strict) {  // final E-step against the last centres
         for (int j = tid; j < K; j += NT) {
-          double s = 0.0;
-          for (int k = 0; k < d; ++k) s += cen[static_cast<size_t>(j) * d + k] * cen[static_cast<size_t>(j) * d + k];
-          s_red[j] = s;
+          const double* cj = cen + static_cast<size_t>(j) * d;
+          s_red[j] = einsum_sq([&](int k) { return cj[k]; }, d);
         }
         __syncthreads();
         for (int r = tid; r < m; r += NT) {
