@@ -1456,7 +1456,9 @@ struct Lay4 {
   static constexpr int RING = NRING4 * SLOT;
   static constexpr int S_BYTES = CW * DP * 4;                 // centre sums [CW][DP] f32 (aliases the ring)
   static constexpr int OFF_POT = RING;                         // seeding partials [NW][16][64] f32
-  static constexpr int POT_END = RING + NW * 16 * 64 * 4;
+  static constexpr int OFF_IAC = OFF_POT + NW * 16 * 64 * 4;   // inertia partials [NW][NCH][64] f32
+  static constexpr int OFF_PRE = OFF_IAC + NW * NCH * 64 * 4;  // closest distances [NW][3][4][64] f32
+  static constexpr int POT_END = OFF_PRE + NW * 3 * 4 * 64 * 4;
   static constexpr int U_END = POT_END > S_BYTES ? POT_END : S_BYTES;
   static constexpr int OFF_LW = (U_END + 15) / 16 * 16;       // labels [NW][2][NCH][RT] u8
   static constexpr int OFF_XN = OFF_LW + NW * 2 * NCH * RT;   // row norms [NRING4][64] f32
@@ -1603,8 +1605,10 @@ struct Wave4 {
 template <int DP>
 __device__ __forceinline__ void estep4(const KArgs& a, const Wave4& W, int te, int lane, const v16f& acc,
                                        const float* cnw, float xn, uint8_t* lw, float* dbuf, int T1,
-                                       const float (&pre)[4], float (&iacc)[NCH], float* pot) {
-  const int r = lane & 31, hh = lane >> 5;
+                                       const float* pre, float* iac, float* pot) {
+  int ln = lane;
+  asm volatile("" : "+v"(ln));  // per-lane constants recomputed per tile rather than held
+  const int r = ln & 31, hh = ln >> 5;
   const int erow = te * RT + r;
   const bool eok = erow < a.m;
   float bm = 0.f;  // running (min, slot) of the Lloyd problem being merged, in chunk order
@@ -1654,7 +1658,7 @@ __device__ __forceinline__ void estep4(const KArgs& a, const Wave4& W, int te, i
           const int lab = bi - static_cast<int>((W.cw[c] >> 8) & 0xFFu);
           if (hh == 0) {
             lw[c * RT + r] = eok ? static_cast<uint8_t>(lab) : static_cast<uint8_t>(0xFF);
-            if (eok) iacc[c] += xn + bm;
+            if (eok) iac[c * 64] += xn + bm;
           }
         }
       }
@@ -1666,11 +1670,12 @@ __device__ __forceinline__ void estep4(const KArgs& a, const Wave4& W, int te, i
       if (mine && eok) {
         const int sslot = w & 31, cs = (w >> 5) & 7, t0 = (w >> 8) & 7, ncol = (w >> 11) & 7;
         const bool seed = (w >> 14) & 1u;
+        const float cl = pre[g * 64];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (j >= ncol) break;
           const float dist = fmaxf(xn + d[j], 0.f);
-          const float dm = seed ? fminf(pre[g], dist) : dist;
+          const float dm = seed ? fminf(cl, dist) : dist;
           const int t = t0 + j;
           const int ws = seed ? ((t < cs) ? t : t + 1) : 0;
           dbuf[(static_cast<size_t>(sslot) * T1 + ws) * a.lsm + erow] = dm;
@@ -1681,34 +1686,36 @@ __device__ __forceinline__ void estep4(const KArgs& a, const Wave4& W, int te, i
   }
 }
 
-// Closest distances of this lane's seeding chunks for tile tp (loaded one tile ahead).
+// Closest distances of this lane's seeding chunks for tile tp, loaded by LDS-DMA into the wave's
+// buffer dst[g * 64 + lane] (one global_load_lds_dword per seeding register group; lanes with
+// nothing to load fetch a harmless dummy word).  Completion: the end-of-tile DMA wait.
 __device__ __forceinline__ void prefetch4(const KArgs& a, const Wave4& W, int tp, int lane, const float* dbuf,
-                                          int T1, float (&pre)[4]) {
+                                          int T1, float* dst) {
   const int hh = lane >> 5;
   const int row = tp * RT + (lane & 31);
   const bool ok = tp < a.T && row < a.m;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    pre[g] = 0.f;
-    if (((W.smask >> (2 * g)) & 3u) == 0) continue;
+    if (((W.smask >> (2 * g)) & 3u) == 0) continue;  // wave-uniform
     const bool mine = (W.smask >> (2 * g + hh)) & 1u;
     unsigned w = hh ? W.cw[2 * g + 1] : W.cw[2 * g];
     asm volatile("" : "+v"(w));
-    if (mine && ok && ((w >> 14) & 1u))
-      pre[g] = dbuf[(static_cast<size_t>(w & 31) * T1 + ((w >> 5) & 7)) * a.lsm + row];
+    const bool load = mine && ok && ((w >> 14) & 1u);
+    const float* src = load ? dbuf + (static_cast<size_t>(w & 31) * T1 + ((w >> 5) & 7)) * a.lsm + row : dbuf;
+    dma_piece(src, dst + g * 64, 4);
   }
 }
 
 // Add the f32 partials into the items' f64 accumulators (one contributing half per item: half 0
 // for Lloyd problems, the chunk's half for seeding columns) and restart them.
-__device__ __forceinline__ void flush4(State4& S, const Wave4& W, int lane, float (&iacc)[NCH], float* pot) {
+__device__ __forceinline__ void flush4(State4& S, const Wave4& W, int lane, float* iac, float* pot) {
   const int r = lane & 31, hh = lane >> 5;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     if (!((W.lend >> c) & 1u)) continue;
-    const double v = half_sum(static_cast<double>(iacc[c]));
+    const double v = half_sum(static_cast<double>(iac[c * 64]));
     if (r == 0 && hh == 0) S.iinert[(W.cw[c] >> 16) & 0xFF] += v;
-    iacc[c] = 0.f;
+    iac[c * 64] = 0.f;
   }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -1863,12 +1870,13 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
       const int lp = static_cast<int>(S.cword[wave][lcq] & 0x3Fu);
       uint8_t* lgl = glab + static_cast<size_t>(lst ? lp : 0) * a.lsm + lrq;
       bool chg = false;
-      float iacc[NCH];
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) iacc[c] = 0.f;
       float* pot = reinterpret_cast<float*>(smem + LY::OFF_POT) + wave * (16 * 64) + lane;
+      float* iac = reinterpret_cast<float*>(smem + LY::OFF_IAC) + wave * (NCH * 64) + lane;
+      float* prebuf = reinterpret_cast<float*>(smem + LY::OFF_PRE) + wave * (3 * 4 * 64);  // [3][4][64]
 #pragma unroll
       for (int v = 0; v < 16; ++v) pot[v * 64] = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) iac[c * 64] = 0.f;
       // pipeline prologue: tile 0 in the ring, indices of tile 1; operands of tile 0
       TileIdx<DP> nI;
       {
@@ -1876,66 +1884,56 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
         idx_issue<DP>(a, idx, 0, wave, lane, I0);
         tile_dma<DP>(a, I0, ring, XN, wave, lane);
         idx_issue<DP>(a, idx, RT, wave, lane, nI);
+        prefetch4(a, W, 0, lane, dbuf, T1, prebuf);
         dma_wait();
       }
-      float pre[4];
-      prefetch4(a, W, 0, lane, dbuf, T1, pre);
       unsigned lold = lst ? *reinterpret_cast<const unsigned*>(lgl) : 0u;
       __syncthreads();  // cnorm, iinert, tile 0
       const float* cnw = S.cnorm + 32 * wave;
 #ifdef CC_KM_STAMPS
       unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-      for (int t = 0; t < T; ++t) {
-        KM_STAMP(s0);
-        // gather: rows of tile t+1 by LDS-DMA (indices loaded last iteration), indices of t+2;
-        // operands of tile t+1
-        if (t + 1 < T) tile_dma<DP>(a, nI, ring + ((t + 1) % NRING4) * LY::SLOT, XN + ((t + 1) % NRING4) * 64, wave, lane);
-        if (t + 2 < T) idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
-        float npre[4];
-        prefetch4(a, W, t + 1, lane, dbuf, T1, npre);
-        const unsigned nlold = (lst && t + 1 < T) ? *reinterpret_cast<const unsigned*>(lgl + (t + 1) * RT) : 0u;
-        __builtin_amdgcn_sched_barrier(0);
-        KM_STAMP(s1);
+      // distances of tile t (the v3 MFMA sequence) into acc
+      auto dist = [&](int t, v16f& acc) __attribute__((always_inline)) {
         const char* xs = ring + (t % NRING4) * LY::SLOT;
-        uint8_t* lw = lwave + (t & 1) * (NCH * RT);
-        if (tact) {
-          // distances of tile t (MFMA, the v3 sequence)
-          v16f acc = {};
-          {
-            int lro = lr;
-            asm volatile("" : "+v"(lro));
-            h8 bh = *reinterpret_cast<const h8*>(xs + xoff<DP>(lro, hh));
-            h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + xoff<DP>(lro, hh));
+        acc = v16f{};
+        int lro = lr;
+        asm volatile("" : "+v"(lro));
+        h8 bh = *reinterpret_cast<const h8*>(xs + xoff<DP>(lro, hh));
+        h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + xoff<DP>(lro, hh));
 #pragma unroll
-            for (int s = 0; s < DP / 16; ++s) {
-              h8 nh = bh, nl = bl;
-              if (s + 1 < DP / 16) {
-                const int off = xoff<DP>(lro, 2 * (s + 1) + hh);
-                nh = *reinterpret_cast<const h8*>(xs + off);
-                nl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
-              }
-              acc = mfma16(ah[s], bl, acc);
-              acc = mfma16(al[s], bh, acc);
-              acc = mfma16(ah[s], bh, acc);
-              __builtin_amdgcn_sched_barrier(0);
-              bh = nh;
-              bl = nl;
-            }
+        for (int s = 0; s < DP / 16; ++s) {
+          h8 nh = bh, nl = bl;
+          if (s + 1 < DP / 16) {
+            const int off = xoff<DP>(lro, 2 * (s + 1) + hh);
+            nh = *reinterpret_cast<const h8*>(xs + off);
+            nl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
           }
-          KM_STAMP(s2i);
-          KM_ACC(1, s1, s2i);
-          const float xn = XN[(t % NRING4) * 64 + lr];
-          estep4<DP>(a, W, t, lane, acc, cnw, xn, lw, dbuf, T1, pre, iacc, pot);
+          acc = mfma16(ah[s], bl, acc);
+          acc = mfma16(al[s], bh, acc);
+          acc = mfma16(ah[s], bh, acc);
+          __builtin_amdgcn_sched_barrier(0);
+          bh = nh;
+          bl = nl;
         }
+      };
+      // E-step of tile te from acc
+      auto estep_of = [&](int te, const v16f& acc) __attribute__((always_inline)) {
+        const float xn = XN[(te % NRING4) * 64 + lr];
+        estep4<DP>(a, W, te, lane, acc, cnw, xn, lwave + (te & 1) * (NCH * RT), dbuf, T1,
+                   prebuf + (te % 3) * (4 * 64) + lane, iac, pot);
         __builtin_amdgcn_wave_barrier();
-        KM_STAMP(s3);
-        // M-step of tile t (one-hot x X on f16 MFMA; counts by popcount)
+      };
+      // M-step of tile tm (one-hot x X on f16 MFMA; counts by popcount), its label store (old
+      // label word lo) and the flush of the partials
+      auto mstep = [&](int tm, unsigned lo) __attribute__((always_inline)) {
+        const char* xs = ring + (tm % NRING4) * LY::SLOT;
+        const uint8_t* lw = lwave + (tm & 1) * (NCH * RT);
         if (mact) {
           const uint8_t* lsb = lw + myend * RT;
-          int lanel = lane;
-          asm volatile("" : "+v"(lanel));
-          const int G = lanel >> 4, q = (lanel >> 2) & 3, pp = lanel & 3;
+          int ln = lane;
+          asm volatile("" : "+v"(ln));  // recompute the transposed-read offsets per tile
+          const int G = ln >> 4, q = (ln >> 2) & 3, pp = ln & 3;
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
             const unsigned long long lab8 = *reinterpret_cast<const unsigned long long*>(lsb + 16 * s2 + 8 * hh);
@@ -1975,32 +1973,85 @@ __global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
             }
           }
         }
-        KM_STAMP(s4);
-        // labels of tile t: compare with the previous sweep's, store (one dword = 4 rows per lane)
-        if (lst) {
+        if (lst) {  // labels of tile tm vs the previous sweep's; store (one dword = 4 rows per lane)
           const unsigned w32 = *reinterpret_cast<const unsigned*>(lw + lcq * RT + lrq);
-          chg |= (w32 != lold);
-          *reinterpret_cast<unsigned*>(lgl + t * RT) = w32;
+          chg |= (w32 != lo);
+          *reinterpret_cast<unsigned*>(lgl + tm * RT) = w32;
         }
-        if ((t % FLUSH) == FLUSH - 2) flush4(S, W, lane, iacc, pot);  // the v3 flush windows
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pre[i] = npre[i];
-        lold = nlold;
-        dma_wait();
-        KM_STAMP(s5);
-        __syncthreads();
-        KM_STAMP(s6);
-        KM_ACC(0, s0, s1);
-        KM_ACC(2, s1, s3);  // distances + E-step (the distance share is stamp 1 of active waves)
-        KM_ACC(3, s3, s4);
-        KM_ACC(4, s4, s5);
-        KM_ACC(5, s5, s6);
+        if ((tm % FLUSH) == FLUSH - 2) flush4(S, W, lane, iac, pot);  // the v3 flush windows
+      };
+      // gather of tile t+1 (LDS-DMA rows, row norms, closest distances), indices of tile t+2
+      auto issue = [&](int t) __attribute__((always_inline)) {
+        if (t + 1 < T) {
+          tile_dma<DP>(a, nI, ring + ((t + 1) % NRING4) * LY::SLOT, XN + ((t + 1) % NRING4) * 64, wave, lane);
+          prefetch4(a, W, t + 1, lane, dbuf, T1, prebuf + ((t + 1) % 3) * (4 * 64));
+        }
+        if (t + 2 < T) idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
+      };
+      // Waves w and w + 4 share a SIMD.  Waves 0-3 run distances(t) -> E-step(t) -> M-step(t);
+      // waves 4-7 lag one tile, E-step(t-1) -> M-step(t-1) -> distances(t), so that one wave's
+      // E-step vector work overlaps its partner's distance MFMAs.  Every result is the same
+      // either way; the ring keeps tile t-1 until iteration t+1.  Both loops pass T + 1 barriers.
+      if (wave < NW / 2) {
+        for (int t = 0; t <= T; ++t) {
+          KM_STAMP(s0);
+          issue(t);
+          const unsigned nlold = (lst && t + 1 < T) ? *reinterpret_cast<const unsigned*>(lgl + (t + 1) * RT) : 0u;
+          KM_STAMP(s1);
+          if (t < T) {
+            v16f acc;
+            if (tact) dist(t, acc);
+            KM_STAMP(s2);
+            KM_ACC(1, s1, s2);
+            if (tact) estep_of(t, acc);
+            KM_STAMP(s3);
+            KM_ACC(2, s2, s3);
+            mstep(t, lold);
+            KM_STAMP(s4);
+            KM_ACC(3, s3, s4);
+          }
+          lold = nlold;
+          KM_STAMP(s5);
+          dma_wait();
+          __syncthreads();
+          KM_STAMP(s6);
+          KM_ACC(0, s0, s1);
+          KM_ACC(4, s5, s6);
+        }
+      } else {
+        v16f acc = {};
+        unsigned lold1 = 0u;
+        for (int t = 0; t <= T; ++t) {
+          KM_STAMP(s0);
+          issue(t);
+          const unsigned nlold = (lst && t + 1 < T) ? *reinterpret_cast<const unsigned*>(lgl + (t + 1) * RT) : 0u;
+          KM_STAMP(s1);
+          if (t >= 1) {
+            if (tact) estep_of(t - 1, acc);
+            KM_STAMP(s2);
+            KM_ACC(2, s1, s2);
+            mstep(t - 1, lold1);
+            KM_STAMP(s3);
+            KM_ACC(3, s2, s3);
+          }
+          KM_STAMP(s4);
+          if (t < T && tact) dist(t, acc);
+          KM_STAMP(s5);
+          KM_ACC(1, s4, s5);
+          lold1 = lold;
+          lold = nlold;
+          dma_wait();
+          __syncthreads();
+          KM_STAMP(s6);
+          KM_ACC(0, s0, s1);
+          KM_ACC(4, s5, s6);
+        }
       }
 #ifdef CC_KM_STAMPS
       if (blockIdx.x == 0 && lane == 0 && a.stats)
         for (int k = 0; k < 7; ++k) atomicAdd(&a.stats[8 + 8 * wave + k], st_acc[k]);
 #endif
-      flush4(S, W, lane, iacc, pot);
+      flush4(S, W, lane, iac, pot);
       // labels changed, per Lloyd problem of this wave
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
