@@ -1497,6 +1497,25 @@ __device__ void schedule4(const KArgs& a, State4& S, const int32_t* idx) {
   }
   int ni = 0;
   unsigned long long nseed = 0, nlloyd = 0, nm = 0;
+  // Dense packing: the chunk demand of the sweep decides how many waves are active (an idle
+  // wave skips its distances, E- and M-step); items go worst-fit among the active waves, and a
+  // further wave is opened only when an item fits none of them.
+  int demand = 0;
+  for (int p = 0; p < P; ++p) {
+    if (S.st[p] == ST_SEED) demand += ((S.c[p] == 0 ? 1 : S.ntr[p]) + 3) / 4;
+    else if (S.st[p] == ST_RUN || S.st[p] == ST_FINAL) demand += (S.K[p] + 3) / 4;
+  }
+  int A = min(NW, max(1, (demand + NCH - 1) / NCH));
+  auto pick = [&](int nch) {
+    int w = -1;
+    for (int q = 0; q < A; ++q)
+      if (hi[q] - lo[q] >= nch && (w < 0 || hi[q] - lo[q] > hi[w] - lo[w])) w = q;
+    while (w < 0 && A < NW) {
+      ++A;
+      if (hi[A - 1] - lo[A - 1] >= nch) w = A - 1;
+    }
+    return w;
+  };
   for (int p = 0; p < P; ++p) S.pitem[p] = -1;
   for (int p = 0; p < P; ++p) {
     if (S.st[p] != ST_SEED) continue;
@@ -1504,9 +1523,7 @@ __device__ void schedule4(const KArgs& a, State4& S, const int32_t* idx) {
     const int nt = (c == 0) ? 1 : S.ntr[p];
     const int nch = (nt + 3) / 4;
     if (ni + nt > IMAX) continue;
-    int w = -1;
-    for (int q = 0; q < NW; ++q)
-      if (hi[q] - lo[q] >= nch && (w < 0 || hi[q] - lo[q] > hi[w] - lo[w])) w = q;
+    const int w = pick(nch);
     if (w < 0) continue;
     S.pitem[p] = static_cast<short>(ni);
     const int kind = (c == 0) ? IK_SEED0 : IK_SEED;
@@ -1541,10 +1558,7 @@ __device__ void schedule4(const KArgs& a, State4& S, const int32_t* idx) {
     const int st = S.st[p];
     if (st != ST_RUN && st != ST_FINAL) continue;
     const int K = S.K[p], nch = (K + 3) / 4;
-    int w = -1;
-    if (ni + 1 <= IMAX)
-      for (int q = 0; q < NW; ++q)
-        if (hi[q] - lo[q] >= nch && (w < 0 || hi[q] - lo[q] > hi[w] - lo[w])) w = q;
+    const int w = (ni + 1 <= IMAX) ? pick(nch) : -1;
     if (w < 0) {
       if (first_skip < 0) first_skip = p;
       continue;
@@ -2530,10 +2544,11 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
   a.seedmax = seedmax;
   a.lsm = (m + 63) & ~63;
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nU));
-  // Engine v4 (wave-local problems) when every K fits one wave's 32 slots; v3 otherwise.
-  // CCMI_KM_ENGINE=3 forces v3 (diagnostics: the two engines give bit-identical results).
+  // Engine v3 by default.  CCMI_KM_ENGINE=4 selects v4 (wave-local problems, K <= 32): the two
+  // engines give bit-identical results; v4 measured slower at C3 (3.51 s vs 2.50 s, see
+  // DESIGN.md section 3) and is kept as the tested alternative schedule.
   const char* eng = std::getenv("CCMI_KM_ENGINE");
-  const bool v4 = kmax <= KMAX4 && !(eng && eng[0] == '3');
+  const bool v4 = kmax <= KMAX4 && eng && eng[0] == '4';
   switch (dpad) {
     case 32: launch<32>(a, blocks, st, v4); break;
     case 64: launch<64>(a, blocks, st, v4); break;

@@ -9,7 +9,9 @@
 //   * tol = mean(var(X_sub, axis=0)) * tol_rel (_tolerance; numpy pairwise mean over features);
 //   * k-means++ (_kmeans_plusplus): squared distances ((-2 x.c) + |c|^2) + |x|^2 clipped at 0
 //     (_euclidean_distances), candidates by searchsorted over the float64 cumsum, the
-//     candidate with the lowest potential kept;
+//     candidate with the lowest potential kept, the potentials in OpenBLAS's ddot / dgemv_t
+//     orders (single-threaded; above numpy's BLAS threading threshold the order depends on
+//     the host's thread count and is not reproduced);
 //   * squared norms of rows and centres in numpy einsum's order (row_norms);
 //   * Lloyd (_kmeans_single_lloyd / lloyd_iter_chunked_dense): distances |c|^2 - 2 x.c,
 //     argmin with strict < (lowest index on ties), centre sums in row order, empty clusters
@@ -125,6 +127,74 @@ __device__ __forceinline__ double euclid4(const double* a, const double* b, int 
   return res;
 }
 
+// The k-means++ potentials are BLAS reductions of the closest distances with unit weights.
+// Their orders were measured against the scipy-openblas build (OpenBLAS 0.3.29, DYNAMIC_ARCH,
+// SkylakeX/Haswell kernels, one thread) that numpy uses in this image; with unit weights the
+// products are exact, so each reduction is a fixed tree of additions.
+//
+// current_pot = closest_dist_sq @ sample_weight (a (1, m) @ (m,) product, numpy -> ddot):
+// 16-element blocks; the first multiple of 32 in four 8-lane accumulators (each folded to 4 lanes,
+// low half + high half), a 16-element remainder into four 4-lane accumulators, the accumulators
+// summed ((a0 + a1) + a2) + a3, the lanes (q0 + q2) + (q1 + q3), then the tail sequentially.
+__device__ double blas_ddot_ones(const double* x, int n) {
+  const int n1 = n & -16, n32 = n1 & ~31;
+  double A[4][4];
+  {
+    double Z[4][8];
+    for (int a = 0; a < 4; ++a)
+      for (int q = 0; q < 8; ++q) Z[a][q] = 0.0;
+    for (int i = 0; i < n32; i += 32)
+      for (int a = 0; a < 4; ++a)
+        for (int q = 0; q < 8; ++q) Z[a][q] += x[i + 8 * a + q];
+    for (int a = 0; a < 4; ++a)
+      for (int q = 0; q < 4; ++q) A[a][q] = Z[a][q] + Z[a][q + 4];
+  }
+  for (int i = n32; i < n1; i += 16)
+    for (int a = 0; a < 4; ++a)
+      for (int q = 0; q < 4; ++q) A[a][q] += x[i + 4 * a + q];
+  double L[4];
+  for (int q = 0; q < 4; ++q) L[q] = ((A[0][q] + A[1][q]) + A[2][q]) + A[3][q];
+  double dot = (L[0] + L[2]) + (L[1] + L[3]);
+  for (int i = n1; i < n; ++i) dot += x[i];
+  return dot;
+}
+
+// candidates_pot = distance_to_candidates @ sample_weight.reshape(-1, 1) ((ntr, m) @ (m, 1),
+// numpy -> dgemv_t over ntr columns of length m).  Rows m & ~3 in blocks of 2048, each block's
+// column sum added to y; columns in groups of 4 use 4-lane accumulators (lanes (q0 + q2) +
+// (q1 + q3)), a pair of remaining columns 2 lanes (l0 + l1), a last odd column 4 lanes; the
+// m & 3 tail rows are summed left to right and added last.
+__device__ double blas_gemv_t_ones(const double* x, int m, int col, int ncol) {
+  const int n4 = ncol & ~3, rem = ncol - n4;
+  const bool two = rem >= 2 && col >= n4 && col < n4 + 2;
+  const int m1 = m & ~3;
+  double y = 0.0;
+  for (int b = 0; b < m1; b += 2048) {
+    const int e = b + 2048 < m1 ? b + 2048 : m1;
+    double s;
+    if (two) {
+      double l0 = 0.0, l1 = 0.0;
+      for (int i = b; i < e; i += 2) {
+        l0 += x[i];
+        l1 += x[i + 1];
+      }
+      s = l0 + l1;
+    } else {
+      double l[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int i = b; i < e; i += 4)
+        for (int q = 0; q < 4; ++q) l[q] += x[i + q];
+      s = (l[0] + l[2]) + (l[1] + l[3]);
+    }
+    y += s;
+  }
+  if (m1 < m) {
+    double t = x[m1];
+    for (int i = m1 + 1; i < m; ++i) t += x[i];
+    y += t;
+  }
+  return y;
+}
+
 struct WG {
   double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew;
   int32_t *lab, *lold;
@@ -213,11 +283,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
         w.cl[r] = dd > 0.0 ? dd : 0.0;
       }
       __syncthreads();
-      if (tid == 0) {
-        double pot = 0.0;
-        for (int r = 0; r < m; ++r) pot += w.cl[r];
-        s_pot[0] = pot;
-      }
+      if (tid == 0) s_pot[0] = blas_ddot_ones(w.cl, m);
       __syncthreads();
       double pot = s_pot[0];
       for (int c = 1; c < K; ++c) {
@@ -247,11 +313,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
           }
         }
         __syncthreads();
-        if (tid < ntr) {
-          double s = 0.0;
-          for (int r = 0; r < m; ++r) s += w.dc[static_cast<size_t>(tid) * m + r];
-          s_pot[tid] = s;
-        }
+        if (tid < ntr) s_pot[tid] = blas_gemv_t_ones(w.dc + static_cast<size_t>(tid) * m, m, tid, ntr);
         __syncthreads();
         int bt = 0;
         for (int t = 1; t < ntr; ++t)

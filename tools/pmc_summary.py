@@ -8,7 +8,7 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 vals = collections.defaultdict(float)
 for f in sorted(glob.glob(f"{root}/p*/p*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if "kmeans_kernel" in r["Kernel_Name"]:
+        if "kmeans" in r["Kernel_Name"] and "_kernel" in r["Kernel_Name"] and "split" not in r["Kernel_Name"]:
             vals[r["Counter_Name"]] += float(r["Counter_Value"])
 st = eval(open(f"{root}/p1.log").read().split("stats")[1].strip().splitlines()[0])
 w = vals["SQ_WAVES"]
