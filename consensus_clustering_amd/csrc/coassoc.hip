@@ -36,7 +36,9 @@
 
 #include <cstdint>
 #include <cmath>
+#include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "ccmi_internal.h"
 
@@ -242,6 +244,148 @@ __device__ __forceinline__ void expand_chunk(const uint32_t (&w)[32], int kc, ui
   }
 }
 
+// ---- exact-K channel packing (K not a power of two, K <= 32) -------------------------------
+// A super-step holds HS = floor(128 / K) whole resamples at virtual k = h_local * K + c, and
+// the HS*K..127 tail is zero: channels are no longer padded to the next power of two (at C3,
+// K = 2..20, 1720 super-steps per tile instead of 2384).  Step s starts at label byte s * HS,
+// which is not 16-B aligned: each row loads the chunks covering it and shifts them into place
+// by the wave-uniform offset (ExactK::DW).
+// Diagnostic build only (-DCC_CO_STAMPS): per-phase cycles of the co-association workgroups
+// (thread 0 of each), summed into cc_co_stamp_acc: prologue, main loop, epilogue setup,
+// binning, reduction; read with cc_co_stamps().
+#ifdef CC_CO_STAMPS
+__device__ unsigned long long cc_co_stamp_acc[8];
+#define CO_STAMP(var) \
+  __builtin_amdgcn_sched_barrier(0); \
+  const unsigned long long var = __builtin_amdgcn_s_memtime(); \
+  __builtin_amdgcn_sched_barrier(0)
+#define CO_ACC(k, a, b) \
+  if (KP > 1 && threadIdx.x == 0) atomicAdd(&cc_co_stamp_acc[k], (b) - (a))
+#else
+#define CO_STAMP(var)
+#define CO_ACC(k, a, b)
+#endif
+
+// Two load forms, chosen per K by measurement (C3, tools/gpu_co3.sh): for K < 10 aligned 16-B
+// chunks and a dword shift by selects; for K >= 10 dword-aligned 16-B loads from the dword holding
+// the first byte, so only the byte shift remains (fewer VALU where steps are many).
+template <int K>
+struct ExactK {
+  static constexpr int HS = 128 / K;                // resamples per super-step
+  static constexpr int NWX = (HS + 3) / 4;          // aligned label dwords of a step
+  static constexpr bool DW = K >= 10;               // dword-aligned loads
+  static constexpr int NC16 = DW ? (NWX + 1 + 3) / 4 : (HS + 15 + 15) / 16;
+  static constexpr int RAW = 4 * NC16;
+  static_assert(RAW >= NWX + (DW ? 1 : 4), "chunk cover");
+};
+
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// Raw dwords of step s of one row.  Bytes at or past the row's ldl (a multiple of 16) read as
+// 0xFF, and no load goes past the row.
+template <int K>
+__device__ __forceinline__ void load_raw(const uint8_t* rowp, int s, int ldl, bool valid,
+                                         uint32_t (&raw)[ExactK<K>::RAW]) {
+  using E = ExactK<K>;
+  const uint32_t msk = valid ? 0u : 0xFFFFFFFFu;
+  if constexpr (E::DW) {
+    const int a4 = (s * E::HS) & ~3;
+#pragma unroll
+    for (int c = 0; c < E::NC16; ++c) {
+      const int o = a4 + 16 * c;
+      u32x4_a4 v;
+      if (o + 16 <= ldl) {  // wave-uniform
+        v = *reinterpret_cast<const u32x4_a4*>(rowp + o);
+      } else {  // the row's end (last step only): dword by dword
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[q] = (o + 4 * q + 4 <= ldl) ? *reinterpret_cast<const uint32_t*>(rowp + o + 4 * q) : 0xFFFFFFFFu;
+      }
+      raw[4 * c + 0] = v.x | msk;
+      raw[4 * c + 1] = v.y | msk;
+      raw[4 * c + 2] = v.z | msk;
+      raw[4 * c + 3] = v.w | msk;
+    }
+  } else {
+    const int a16 = (s * E::HS) & ~15;
+#pragma unroll
+    for (int c = 0; c < E::NC16; ++c) {  // branch-free: clamped re-reads, masked
+      const int o = a16 + 16 * c;
+      const uint32_t m = (o < ldl) ? msk : 0xFFFFFFFFu;
+      const uint4 v = *reinterpret_cast<const uint4*>(rowp + (o < ldl ? o : ldl - 16));
+      raw[4 * c + 0] = v.x | m;
+      raw[4 * c + 1] = v.y | m;
+      raw[4 * c + 2] = v.z | m;
+      raw[4 * c + 3] = v.w | m;
+    }
+  }
+}
+
+// Label bytes of step s in place (byte h of w = resample s * HS + h); resamples at or past Hpad
+// (the last step's tail) read as 0xFF = not sampled.  The dword shift (16-B form) is a select on
+// the wave-uniform offset (a switch made the compiler spill), the byte shift v_alignbyte.
+template <int K>
+__device__ __forceinline__ void realign(const uint32_t (&raw)[ExactK<K>::RAW], int s, int Hpad,
+                                        uint32_t (&w)[32]) {
+  using E = ExactK<K>;
+  const int off = (s * E::HS) & (E::DW ? 3 : 15);  // wave-uniform
+  const int bsh = off & 3;
+  if constexpr (E::DW) {
+#pragma unroll
+    for (int i = 0; i < E::NWX; ++i) w[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], bsh);
+  } else {
+    const int dsh = off >> 2;
+    auto at = [&](int j) __attribute__((always_inline)) { return j < E::RAW ? raw[j] : 0xFFFFFFFFu; };
+    uint32_t sh[E::NWX + 1];  // dwords dsh .. dsh + NWX of raw
+#pragma unroll
+    for (int i = 0; i <= E::NWX; ++i) {
+      const uint32_t x01 = (dsh & 1) ? at(i + 1) : at(i);
+      const uint32_t x23 = (dsh & 1) ? at(i + 3) : at(i + 2);
+      sh[i] = (dsh & 2) ? x23 : x01;
+    }
+#pragma unroll
+    for (int i = 0; i < E::NWX; ++i) w[i] = __builtin_amdgcn_alignbyte(sh[i + 1], sh[i], bsh);
+  }
+  const int rem = Hpad - s * E::HS;
+  if (rem < E::HS) {  // wave-uniform: the last step
+#pragma unroll
+    for (int i = 0; i < E::NWX; ++i) {
+      const int k = rem - 4 * i;
+      w[i] |= (k >= 4) ? 0u : (k <= 0 ? 0xFFFFFFFFu : (0xFFFFFFFFu << (8 * k)));
+    }
+  }
+}
+
+// Dwords 8 kc .. 8 kc + 7 of the exact-K one-hot: byte j = [label(j / K) == j % K] for
+// j < HS * K, else 0.  Per dword: v_perm gathers the (at most two) label bytes its 4 channels
+// belong to, XOR with the channel numbers, and a carry-free zero-byte test gives the 0/1 bytes.
+template <int K>
+__device__ __forceinline__ void expand_chunk_exact(const uint32_t (&w)[32], int kc, uint32_t (&o)[8]) {
+  using E = ExactK<K>;
+#pragma unroll
+  for (int qq = 0; qq < 8; ++qq) {
+    const int j0 = 4 * (8 * kc + qq);
+    if (j0 >= E::HS * K) {
+      o[qq] = 0u;
+      continue;
+    }
+    const int dA = (j0 / K) >> 2;
+    uint32_t sel = 0, cc = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int j = j0 + b;
+      const bool ok = j < E::HS * K;
+      sel |= static_cast<uint32_t>(ok ? (j / K - 4 * dA) : 0x0C) << (8 * b);
+      cc |= static_cast<uint32_t>(ok ? (j % K) : 0xFE) << (8 * b);
+    }
+    const uint32_t s1 = w[dA];
+    const uint32_t s0 = (dA + 1 < E::NWX) ? w[dA + 1] : s1;
+    const uint32_t x = __builtin_amdgcn_perm(s0, s1, sel) ^ cc;
+    const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    o[qq] = (~(t | x) & 0x80808080u) >> 7;
+  }
+}
+
 template <int KP>
 __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     const uint8_t* __restrict__ labels, int n, int ldl, int Hpad, int64_t tile_begin,
@@ -250,7 +394,9 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     int32_t* __restrict__ full_out, const uint16_t* __restrict__ btab, int bt_rows) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
   constexpr int HS = 128 / KP;  // resamples per super-step
+  constexpr bool EX = (KP & (KP - 1)) != 0;  // exact-K packing (K = KP not a power of two)
 
+  CO_STAMP(st0);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -275,7 +421,7 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
   const int erb = erow >> 5, er = erow & 31;
   char* const wbase = lds + side * SIDE + erb * KC * FRAG + er * 16;
 
-  const int nsteps = Hpad / HS;
+  const int nsteps = EX ? (Hpad + HS - 1) / HS : Hpad / HS;
   v16i acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -288,9 +434,26 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
   constexpr bool PF2 = KP > 1;
   constexpr int NWD = (HS + 3) / 4;
   uint32_t w[32], wn[PF2 ? NWD : 1], o[32];
-  load_labels<KP>(rowp, evalid, w);
-  expand<KP>(w, o);
-  if constexpr (PF2) {
+  constexpr int NRW = EX ? ExactK<EX ? KP : 3>::RAW : 1;
+  uint32_t raw1[NRW];  // exact K: raw chunks of step s+2 (one step in flight; two measured slower)
+  if constexpr (EX) {
+    load_raw<KP>(rowp, 0, ldl, evalid, raw1);
+    realign<KP>(raw1, 0, Hpad, w);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      uint32_t oc[8];
+      expand_chunk_exact<KP>(w, kc, oc);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[8 * kc + q] = oc[q];
+    }
+    load_raw<KP>(rowp, nsteps > 1 ? 1 : 0, ldl, evalid, raw1);
+    realign<KP>(raw1, nsteps > 1 ? 1 : 0, Hpad, w);  // step 1
+    load_raw<KP>(rowp, nsteps > 2 ? 2 : 0, ldl, evalid, raw1);  // step 2
+  } else {
+    load_labels<KP>(rowp, evalid, w);
+    expand<KP>(w, o);
+  }
+  if constexpr (PF2 && !EX) {
     load_labels<KP>(rowp + (nsteps > 1 ? HS : 0), evalid, w);  // step 1
     uint32_t t32[32];
     load_labels<KP>(rowp + (nsteps > 2 ? 2 * HS : 0), evalid, t32);  // step 2
@@ -305,6 +468,8 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           make_uint4(o[kc * 8 + g * 4 + 0], o[kc * 8 + g * 4 + 1], o[kc * 8 + g * 4 + 2],
                      o[kc * 8 + g * 4 + 3]);
   __syncthreads();
+  CO_STAMP(st1);
+  CO_ACC(0, st0, st1);
 
   for (int s = 0; s < nsteps; ++s) {
     const bool more = (s + 1) < nsteps;
@@ -341,7 +506,10 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
         // kc's MFMAs issue, so the vector work runs in the MFMA shadows
         // (the stores are unconditional: on the last step they land in the buffer nobody reads)
         uint32_t oc[8];
-        expand_chunk<KP>(w, kc, oc);
+        if constexpr (EX)
+          expand_chunk_exact<KP>(w, kc, oc);
+        else
+          expand_chunk<KP>(w, kc, oc);
 #pragma unroll
         for (int g = 0; g < 2; ++g)
           *reinterpret_cast<uint4*>(wb + kc * FRAG + g * 512) =
@@ -351,12 +519,16 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // up to 6 VALU
+          __builtin_amdgcn_sched_group_barrier(0x002, (EX && KP >= 10) ? 9 : 6, 0);  // VALU per MFMA
         }
         __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);    // the 2 LDS stores
       }
     }
-    if constexpr (PF2) {
+    if constexpr (EX) {
+      // w <- step s+2 (loaded one step ago), raw1 <- step s+3
+      realign<KP>(raw1, (s + 2) < nsteps ? s + 2 : s, Hpad, w);
+      load_raw<KP>(rowp, (s + 3) < nsteps ? s + 3 : s, ldl, evalid, raw1);
+    } else if constexpr (PF2) {
       // rotate the label prefetch: w <- step s+2, wn <- step s+3 (clamped re-reads at the end)
 #pragma unroll
       for (int q = 0; q < NWD; ++q) w[q] = wn[q];
@@ -378,6 +550,8 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
   }
 
   // ---- epilogue ------------------------------------------------------------
+  CO_STAMP(st2);
+  CO_ACC(1, st1, st2);
   const int64_t tl = t - tile_begin;
   const bool diag = (bi == bj);
   const int row0 = bi * T + wr * 128 + 4 * (lane >> 5);
@@ -436,6 +610,8 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
         rtab[r] = r > 0 ? 20.0f * __builtin_amdgcn_rcpf(static_cast<float>(r)) : 0.0f;
     }
     __syncthreads();
+    CO_STAMP(st3);
+    CO_ACC(2, st2, st3);
     const float* rtab = reinterpret_cast<const float*>(lds + BT_OFF + 16 * ((bt_rows * BT_ROW * 2 + 15) / 16));
     const uint4* it4 = reinterpret_cast<const uint4*>(I_tiles_in + tl * (T * T) + 128 * tid);
     // Interior tiles (off the diagonal, every column < n; all but a sliver of the triangle)
@@ -479,6 +655,8 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
         }
       }
     }
+    CO_STAMP(st4);
+    CO_ACC(3, st3, st4);
     // per-bin totals: 16 threads per bin sum its 512 counters from LDS (16-B reads, the 16
     // threads of a bin cover 256 contiguous bytes per read: conflict-free), then reduce
     // within their 16 lanes: one global atomic per bin and tile (20 contended words: keep it
@@ -497,6 +675,8 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
       for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o);
       if (part == 0 && c) atomicAdd(&bin_counts[b], static_cast<unsigned long long>(c));
     }
+    CO_STAMP(st5);
+    CO_ACC(4, st4, st5);
   }
 }
 
@@ -658,7 +838,22 @@ extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int
   const uint8_t* lab = reinterpret_cast<const uint8_t*>(labels_nh);
   int kp = 2;
   while (kp < K) kp <<= 1;
+  // Exact-K packing (ExactK) when it saves enough super-steps: its expansion costs more VALU
+  // per step than the power-of-two form.  CCMI_CO_PACK=pow2 / exact forces one form
+  // (diagnostics; both give identical counts).
+  if (kp != K && K < 32) {
+    const int hs = 128 / K, se = (Hpad + hs - 1) / hs, sp = Hpad / (128 / kp);
+    const char* pk = std::getenv("CCMI_CO_PACK");
+    const bool force_pow2 = pk && pk[0] == 'p', force_exact = pk && pk[0] == 'e';
+    if (force_exact || (!force_pow2 && 4 * se < 3 * sp)) kp = K;
+  }
   switch (kp) {
+#define CC_EXACT(k) case k: launch_tiles<k>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    CC_EXACT(3) CC_EXACT(5) CC_EXACT(6) CC_EXACT(7) CC_EXACT(9) CC_EXACT(10) CC_EXACT(11)
+    CC_EXACT(12) CC_EXACT(13) CC_EXACT(14) CC_EXACT(15) CC_EXACT(17) CC_EXACT(18) CC_EXACT(19)
+    CC_EXACT(20) CC_EXACT(21) CC_EXACT(22) CC_EXACT(23) CC_EXACT(24) CC_EXACT(25) CC_EXACT(26)
+    CC_EXACT(27) CC_EXACT(28) CC_EXACT(29) CC_EXACT(30) CC_EXACT(31)
+#undef CC_EXACT
     case 2: launch_tiles<2>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
     case 4: launch_tiles<4>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
     case 8: launch_tiles<8>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
@@ -669,6 +864,18 @@ extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int
   }
   return launch_status("cc_coassoc");
 }
+
+#ifdef CC_CO_STAMPS
+extern "C" int cc_co_stamps(unsigned long long* out8, int reset) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(cc_co_stamp_acc), 8 * sizeof(unsigned long long)) != hipSuccess)
+    return CC_ERR_HIP;
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cc_co_stamp_acc), z, sizeof(z)) != hipSuccess) return CC_ERR_HIP;
+  }
+  return CC_OK;
+}
+#endif
 
 extern "C" int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stream) {
   if (!M || !I || !C || n <= 0) {

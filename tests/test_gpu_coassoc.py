@@ -171,3 +171,30 @@ def test_bin_table_exhaustive():
               mism.data_ptr(), engine.stream_ptr())
     torch.cuda.synchronize()
     assert mism.tolist() == [0, 0], (rows, mism.tolist())
+
+
+@pytest.mark.parametrize("n,H,frac", [(300, 200, 0.7), (260, 1000, 0.8), (129, 37, 1.0)])
+def test_exact_k_packing_every_k(n, H, frac):
+    """Exact-K channel packing (floor(128/K) resamples per super-step, unaligned label starts,
+    a partial last step) against a float one-hot product, for every K of 2..33 with labels
+    drawn uniformly over all K channels."""
+    dev = engine.require_gpu()
+    rng = np.random.default_rng(n * H)
+    m = int(frac * n)
+    idx = np.stack([rng.permutation(n)[:m] for _ in range(H)]).astype(np.int32)
+    Ks = list(range(2, 34))
+    labs = [rng.integers(0, K, size=(H, m)).astype(np.int32) for K in Ks]
+    L, Hpad = _device_labels(idx, labs, n, H, dev)
+    I, Ms, counts = _run(L, n, Hpad, Ks)
+    I_ref = O.cosample_matrix(idx.astype(np.int64), n)
+    np.testing.assert_array_equal(I, I_ref)
+    iu = np.triu_indices(n, 1)
+    for j, K in enumerate(Ks):
+        oh = np.zeros((n, H * K), np.float32)
+        for h in range(H):
+            oh[idx[h], h * K + labs[j][h]] = 1.0
+        M_ref = (oh @ oh.T).astype(np.int64)
+        np.testing.assert_array_equal(Ms[j], M_ref, err_msg=f"K={K}")
+        C = O.consensus_matrix(M_ref.astype(np.uint16), I_ref.astype(np.uint16))
+        pair, _ = np.histogram(C[iu], bins=20, range=(0, 1))
+        np.testing.assert_array_equal(counts[j], pair, err_msg=f"K={K}")
