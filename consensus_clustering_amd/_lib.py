@@ -51,6 +51,14 @@ SIGNATURES = {
     "cc_kmeans_f64": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp,
                                _c_int, _c_int, _c_int, _c_dbl, _vp, _c_int, _vp, _vp, _c_int, _vp,
                                _vp, _vp, _c_sz, _c_int, _vp]),
+    "cc_kpp_tables": (_c_int, [_vp, _c_int, _c_int, _c_u32, _c_int, _c_int, _vp, _c_int, _vp]),
+    "cc_prepare_rows_scratch_bytes": (_c_sz, [_c_int, _c_int]),
+    "cc_prepare_rows": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "cc_kmeans_fit_workspace_bytes": (_c_sz, [_c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int,
+                                              _c_int]),
+    "cc_kmeans_fit": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
+                               _c_int, _c_int, _c_dbl, _c_u32, _c_int, _vp, _c_int, _vp, _vp, _vp,
+                               _c_sz, _vp]),
 }
 
 _CSRC = os.path.join(_HERE, "csrc")

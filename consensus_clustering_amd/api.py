@@ -168,10 +168,20 @@ class ConsensusClustering:
         if keep == 'auto':
             keep = n <= 20000
 
-        # resampling (CC.py:216-241): every rank draws all H (needed by nobody else, cheap)
+        # resampling (CC.py:216-241): each rank replays only its own resamples [h0, h1); rows
+        # outside the shard stay zero and are never read (the co-sampling counts come from the
+        # merged label matrix, not from the indices)
         h0, h1 = dist.shard(H, rank, W)
-        idx = engine.resample_indices(self.random_state, n, m, 0, H)
-        idx_d = torch.from_numpy(idx).to(dev)
+        own = engine.resample_indices(self.random_state, n, m, h0, h1) if h1 > h0 else None
+        if (h0, h1) == (0, H):
+            idx = own
+            idx_d = torch.from_numpy(idx).to(dev)
+        else:
+            idx = np.zeros((H, m), dtype=np.int32)
+            idx_d = torch.zeros((H, m), dtype=torch.int32, device=dev)
+            if own is not None:
+                idx[h0:h1] = own
+                idx_d[h0:h1] = torch.from_numpy(own).to(dev)
         Hpad = engine.pad_h(H)
         labels = engine.new_label_matrix(max(len(Ks), 1), n, Hpad, dev)
         t_rs = time.perf_counter()
@@ -254,7 +264,8 @@ class ConsensusClustering:
                 res['mij'] = res['iij'] = res['cij'] = None
             self.cdf_at_K_data[K] = res
         self.pair_counts_ = {K: counts_h[k] for k, K in enumerate(Ks)}
-        self.resampling_indices_ = idx
+        self.resampling_indices_ = idx  # rows [h0, h1) of this rank (all of them at W = 1)
+        self.resample_range_ = (h0, h1)
         self.labels_ = labels  # device uint8 [nK, n, Hpad]; 0xFF = not sampled
         self._finish_selection()
         self.timings_ = dict(resample=t_rs - t_start, cluster=t_cl - t_rs,

@@ -13,6 +13,7 @@
 // only after the whole pass: all n-1 draws are replayed.  Resamples are
 // independent streams and run on host threads.
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -132,5 +133,52 @@ extern "C" int cc_random_sample(uint32_t seed, int64_t count, double* out) {
   }
   MT19937 g(seed);
   for (int64_t i = 0; i < count; ++i) out[i] = g.next_double();
+  return CC_OK;
+}
+
+// k-means++ streams of every (K, init) run: sklearn's KMeans(random_state=seed) fit draws, for
+// each of its n_init runs, the first centre with RandomState.choice(m, p=sample_weight/sum)
+// (_kmeans.py:225) and then (K-1) * (2 + floor(ln K)) uniforms, one block of local trials per
+// centre (:243).  Every fit of one K replays RandomState(seed) from the start.  choice with p is
+// numpy's legacy form: p as float64, cdf = cumsum(p) (sequential), cdf /= cdf[-1], one
+// random_sample, searchsorted(side='right').  weight_f64 = 0: unit float32 weights, p = f32(1/m).
+extern "C" int cc_kpp_tables(const int32_t* Ks, int nK, int n_init, uint32_t seed, int m,
+                             int weight_f64, double* kpp_u, int kpp_stride, int32_t* kpp_pos) {
+  if (!Ks || nK <= 0 || n_init <= 0 || m <= 0 || !kpp_u || !kpp_pos) {
+    cc::set_error("cc_kpp_tables: bad arguments");
+    return CC_ERR_ARG;
+  }
+  for (int k = 0; k < nK; ++k) {
+    const int K = Ks[k];
+    const int t = 2 + static_cast<int>(std::log(static_cast<double>(K)));
+    if (K < 1 || 1 + (K - 1) * t > kpp_stride) {
+      cc::set_error("cc_kpp_tables: K out of range or kpp_stride too small");
+      return CC_ERR_ARG;
+    }
+  }
+  const double p = weight_f64 ? 1.0 / static_cast<double>(m)
+                              : static_cast<double>(1.0f / static_cast<float>(m));
+  std::vector<double> cdf(static_cast<size_t>(m));
+  double c = 0.0;
+  for (int i = 0; i < m; ++i) {
+    c += p;
+    cdf[i] = c;
+  }
+  const double last = cdf[m - 1];
+  for (int i = 0; i < m; ++i) cdf[i] /= last;
+  for (int k = 0; k < nK; ++k) {
+    const int K = Ks[k];
+    const int t = 2 + static_cast<int>(std::log(static_cast<double>(K)));
+    MT19937 g(seed);
+    for (int i = 0; i < n_init; ++i) {
+      double* u = kpp_u + (static_cast<size_t>(k) * n_init + i) * kpp_stride;
+      const double r = g.next_double();
+      kpp_pos[k * n_init + i] =
+          static_cast<int32_t>(std::upper_bound(cdf.begin(), cdf.end(), r) - cdf.begin());
+      u[0] = 0.0;
+      for (int j = 0; j < (K - 1) * t; ++j) u[1 + j] = g.next_double();
+      for (int j = 1 + (K - 1) * t; j < kpp_stride; ++j) u[j] = 0.0;
+    }
+  }
   return CC_OK;
 }

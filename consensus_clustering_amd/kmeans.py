@@ -14,6 +14,7 @@ the remaining doubles to the kernel.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -98,24 +99,18 @@ def default_seedmax(m: int) -> int:
 
 
 def kpp_tables(Ks, n_init: int, seed: int, m: int, weight_dtype=np.float32):
-    """k-means++ streams of RandomState(seed) for each (K, init).
+    """k-means++ streams of RandomState(seed) for each (K, init) (native cc_kpp_tables; checked
+    against numpy's own RandomState in tests/test_host_kmeans.py).
 
     Returns (kpp_u [nK, n_init, stride] float64, kpp_pos [nK, n_init] int32, stride).
     kpp_u[k, i, 1 + (c-1)*t + j] is the j-th uniform drawn for centre c of init i.
     """
-    Ks = [int(k) for k in Ks]
-    stride = max(1 + (K - 1) * local_trials(K) for K in Ks)
-    u = np.zeros((len(Ks), n_init, stride), dtype=np.float64)
-    pos = np.zeros((len(Ks), n_init), dtype=np.int32)
-    sw = np.ones(m, dtype=weight_dtype)
-    p = sw / sw.sum()
-    for k, K in enumerate(Ks):
-        t = local_trials(K)
-        rs = np.random.RandomState(seed)
-        for i in range(n_init):
-            pos[k, i] = rs.choice(m, p=p)              # _kmeans.py:225
-            if K > 1:
-                u[k, i, 1:1 + (K - 1) * t] = rs.random_sample((K - 1) * t)  # uniform(size=t) per centre
+    Ks_np = np.ascontiguousarray(np.asarray([int(k) for k in Ks], dtype=np.int32))
+    stride = max(1 + (int(K) - 1) * local_trials(int(K)) for K in Ks_np)
+    u = np.zeros((len(Ks_np), n_init, stride), dtype=np.float64)
+    pos = np.zeros((len(Ks_np), n_init), dtype=np.int32)
+    _lib.call("cc_kpp_tables", Ks_np.ctypes.data, len(Ks_np), int(n_init), ctypes.c_uint32(int(seed)),
+              int(m), int(np.dtype(weight_dtype) == np.float64), u.ctypes.data, stride, pos.ctypes.data)
     return u, pos, stride
 
 
@@ -130,7 +125,8 @@ def scale_exponent(amax: float) -> int:
 
 def prepare_rows(X, device):
     """Mean-centred float32 rows zero-padded to dpad, their squared norms, and the f16 hi/lo
-    MFMA operand image of the rows (cc_split_f16), on device.
+    MFMA operand image of the rows, on device (native cc_prepare_rows, the same preparation
+    cc_kmeans_fit does).
 
     X is a host array or a device tensor (already resident in HBM).  sklearn centres
     X_sub by its own mean (_kmeans.py:1479-1481); distances are translation invariant,
@@ -139,15 +135,17 @@ def prepare_rows(X, device):
     n, d = X.shape
     dpad = dpad_for(d)
     Xt = X if isinstance(X, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(X))
-    Xt = Xt.to(device)
-    mean = Xt.to(torch.float64).mean(dim=0).to(torch.float32)
-    Xd = torch.zeros((n, dpad), dtype=torch.float32, device=device)
-    Xd[:, :d] = Xt.to(torch.float32) - mean
-    xnorm = (Xd * Xd).sum(dim=1).contiguous()
-    e = scale_exponent(float(Xd.abs().max().item()) if n else 0.0)
+    Xt = Xt.to(device=device, dtype=torch.float32).contiguous()
+    Xd = torch.empty((n, dpad), dtype=torch.float32, device=device)
+    xnorm = torch.empty((n,), dtype=torch.float32, device=device)
     Xhl = torch.empty((n, 2, dpad), dtype=torch.int16, device=device)
-    _lib.call("cc_split_f16", Xd.data_ptr(), n, dpad, e, Xhl.data_ptr(), engine.stream_ptr(device))
-    return Xd, xnorm, dpad, Xhl, e
+    lib = _lib.load()
+    scratch = torch.empty(int(lib.cc_prepare_rows_scratch_bytes(n, d)), dtype=torch.uint8, device=device)
+    e = ctypes.c_int(0)
+    _lib.call("cc_prepare_rows", Xt.data_ptr(), n, d, dpad, Xd.data_ptr(), xnorm.data_ptr(),
+              Xhl.data_ptr(), ctypes.byref(e), scratch.data_ptr(), scratch.numel(),
+              engine.stream_ptr(device))
+    return Xd, xnorm, dpad, Xhl, int(e.value)
 
 
 class BatchedKMeans:

@@ -21,6 +21,8 @@
  *   cc_kmeans_batched     CC.py:282 clusterer.fit_predict for every (h, K) at once
  *   cc_kmeans_wide        the same for wide rows (d > 128), as distance/centre GEMM rounds
  *                         (sklearn KMeans: k-means++ init, Lloyd, best of n_init)
+ *   cc_kmeans_f64         the same at float64 for float64 input
+ *   cc_kmeans_fit         CC.py:282 in one call (plans and launches one of the three above)
  */
 #ifndef CCMI_H
 #define CCMI_H
@@ -205,6 +207,47 @@ int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_hm, int H, i
                   const double* kpp_u, int kpp_stride, const int32_t* kpp_pos, uint8_t* labels_nh,
                   int ldl, double* inertia, int32_t* n_iter, void* workspace, size_t ws_bytes,
                   int grid, void* stream);
+
+/* ---- one-call k-means (the advanced entry points above, planned internally) ----------- */
+
+#define CC_KM_FAST 0 /* float32 input: f16 hi/lo MFMA engines (cc_kmeans_batched / _wide) */
+#define CC_KM_F64 1  /* float64 input: cc_kmeans_f64 */
+
+/* k-means++ tables of cc_kmeans_batched for Ks[0..nK) (host): sklearn KMeans(random_state=seed)
+ * replays RandomState(seed) for every K; per init it draws the first centre with
+ * choice(m, p=w/sum(w)) (_kmeans.py:225; unit weights, float32 unless weight_f64) and then
+ * (K-1)*(2+floor(ln K)) uniforms (:243).  kpp_u [nK][n_init][kpp_stride], kpp_pos [nK][n_init]. */
+int cc_kpp_tables(const int32_t* Ks, int nK, int n_init, uint32_t seed, int m, int weight_f64,
+                  double* kpp_u, int kpp_stride, int32_t* kpp_pos);
+
+/* Row image of the float32 engines from raw rows X [n][d] float32 (device): column means
+ * (float64, fixed order), centred rows zero-padded to dpad (Xd [n][dpad]), squared norms
+ * (xnorm [n]), the scale exponent (returned in *scale_exp; synchronises the stream) and the
+ * cc_split_f16 image (Xhl [n][2][dpad]).  scratch: device, cc_prepare_rows_scratch_bytes. */
+size_t cc_prepare_rows_scratch_bytes(int n, int d);
+int cc_prepare_rows(const float* X, int n, int d, int dpad, float* Xd, float* xnorm, uint16_t* Xhl,
+                    int* scale_exp, void* scratch, size_t scratch_bytes, void* stream);
+
+/* Every (resample h in [h_begin, h_end), K, init) k-means fit of a consensus fit in one call:
+ * the loop of clusterer.fit_predict(X[indices]) at CC.py:282 for the default KMeans(n_init)
+ * clusterer.  Plans units, grid and seedmax, builds the k-means++ tables and the row image, and
+ * runs cc_kmeans_batched (d <= 128), cc_kmeans_wide (d > 128) or cc_kmeans_f64.
+ *  X        device [n][d] raw rows: float32 (CC_KM_FAST) or float64 (CC_KM_F64)
+ *  idx_hm   device [H][m] int32 resample rows (rows outside [h_begin, h_end) are not read)
+ *  Ks       host [nK], 1 <= K <= min(127, m)
+ *  labels_nh device [nK][n][ldl] uint8, pre-filled 0xFF; labels_nh[k][idx[h][r]][h]
+ *  inertia  optional device [nK][H] (float32 for CC_KM_FAST, float64 for CC_KM_F64)
+ *  n_iter   optional device [nK][H] int32
+ *  workspace device, ws_bytes >= cc_kmeans_fit_workspace_bytes(...) (less is fine for the
+ *           persistent grid, which shrinks to fit; too little for one workgroup is an error)
+ * Synchronous with respect to the host (it reads max|X| and, for wide rows, a counter per
+ * round).  Results are identical to driving the advanced entry points with the same inputs. */
+size_t cc_kmeans_fit_workspace_bytes(int n, int d, int m, int nh, const int32_t* Ks, int nK,
+                                     int n_init, int precision);
+int cc_kmeans_fit(const void* X, int n, int d, const int32_t* idx_hm, int H, int m, int h_begin,
+                  int h_end, const int32_t* Ks, int nK, int n_init, int max_iter, double tol_rel,
+                  uint32_t seed, int precision, uint8_t* labels_nh, int ldl, void* inertia,
+                  int32_t* n_iter, void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -72,3 +72,19 @@ def test_scale_exponent():
     for amax in (1e-3, 0.7, 1.0, 3.0, 1e4, 6e4):
         e = kmeans.scale_exponent(amax)
         assert amax * 2.0 ** e <= 2 ** 14 and amax * 2.0 ** (e + 1) > 2 ** 14
+
+
+@pytest.mark.parametrize("m,dtype", [(23, np.float64), (8001, np.float32), (40000, np.float32),
+                                     (160000, np.float32), (99991, np.float64)])
+def test_native_kpp_first_centre_matches_numpy_choice(m, dtype):
+    """cc_kpp_tables' first-centre draw is numpy's legacy choice(m, p=w/w.sum()) bit for bit
+    (float64 cumsum of the float32 or float64 p, searchsorted right), for every K's replay."""
+    Ks = [2, 3, 11, 20, 127]
+    u, pos, _ = kmeans.kpp_tables(Ks, 3, 7, m, dtype)
+    sw = np.ones(m, dtype=dtype)
+    for k, K in enumerate(Ks):
+        rs = np.random.RandomState(7)
+        t = kmeans.local_trials(K)
+        for i in range(3):
+            assert pos[k, i] == rs.choice(m, p=sw / sw.sum())
+            np.testing.assert_array_equal(u[k, i, 1:1 + (K - 1) * t], rs.random_sample((K - 1) * t))
