@@ -1387,928 +1387,6 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
   }
 }
 
-// ================================================================================================
-// Engine v4 (units whose K are all <= 32): wave-local problems, distances never leave registers.
-//
-// The sweep is the v3 sweep (same row gather, same f16 hi/lo distance MFMAs, same M-step MFMAs,
-// same f32 partials and flush windows, hence bit-identical labels, inertias and potentials), with
-// the E-step moved into the wave that computed the distances:
-//   * packing: a wave's 32 slots are 8 CHUNKS of 4.  A Lloyd problem occupies ceil(K/4)
-//     consecutive chunks of ONE wave (K padded with +inf dummy slots); a seeding problem's trial
-//     columns occupy whole chunks of one wave (one problem per chunk);
-//   * E-step: each lane (tile row r, half hh) holds 16 distances, one chunk per register group g
-//     (chunk 2g + hh); it takes the per-chunk first argmin, swaps the 4 chunk results with the
-//     other half (v_permlane32_swap), so both halves see all 8 chunks, and merges the chunks of
-//     each problem in slot order (wave-uniform chunk masks): no distance tile in LDS, no LDS
-//     round trip and no dependence on other waves;
-//   * the M-step of the same tile reads the labels the wave itself just wrote (wave-private LDS);
-//   * "labels changed" is detected while the labels are stored (old label word prefetched one
-//     tile ahead, compared, overwritten: one label buffer per problem).
-// One barrier per 32-row tile remains, for the shared row ring.
-constexpr int NCH = 8;      // 4-slot chunks per wave
-constexpr int KMAX4 = 32;   // largest K of a v4 unit (one wave's slots)
-constexpr int NRING4 = 3;   // X tile ring: t+1 (gather), t (distances, M-step), t-1 (lagging waves)
-
-struct State4 {
-  // unit
-  int unit, P;
-  float tol;
-  int rr;
-  unsigned seedfree;
-  // problems
-  unsigned char K[PMAX], kidx[PMAX], init[PMAX], ntr[PMAX], st[PMAX], c[PMAX], cs[PMAX], sslot[PMAX];
-  unsigned char need_sel[PMAX], to_run[PMAX], sbest[PMAX];
-  short cenoff[PMAX], pitem[PMAX];
-  int iter[PMAX], amax[PMAX], nempty[PMAX];
-  float pot32[PMAX], inert[PMAX];
-  int cand[PMAX][TMAX];
-  // sweep
-  int nitems, ncols;
-  unsigned char ikind[IMAX], iprob[IMAX], itr[IMAX];
-  short ioff[IMAX], incol[IMAX];
-  double iinert[IMAX];
-  unsigned ichanged[IMAX];
-  short sitem[CW], scl[CW];
-  unsigned char send[CW];  // end chunk (in its wave) of the slot's Lloyd problem
-  int srow[CW];            // >= 0: X row (seeding candidate); < 0: -(centre row) - 1; INT_MIN: dummy
-  alignas(16) float cnorm[CW];
-  float shift[CW];
-  unsigned cnt[CW];
-  // per wave: chunk masks (bits 0-7 Lloyd, 8-15 Lloyd start, 16-23 Lloyd end, 24-31 seeding) and
-  // one descriptor word per chunk:
-  //   Lloyd chunk:   problem | start slot (in the wave) << 8 | item << 16
-  //   seeding chunk: seeding slot | closest slot << 5 | first trial << 8 | columns << 11 |
-  //                  kind (1 = SEED, 0 = SEED0) << 14 | item of the first trial << 16
-  unsigned wmask[NW];
-  unsigned cword[NW][NCH];
-  // scratch
-  double red_v[NW];
-  int red_i[NW];
-  int map[KMAX + 1];
-  int flag;
-  unsigned long long n_lloyd, n_seed, n_mrows, n_reloc, n_sweeps, n_ctiles;
-};
-
-template <int DP>
-struct Lay4 {
-  static constexpr int IMG = RT * DP * 2;
-  static constexpr int SLOT = 2 * IMG;
-  static constexpr int RING = NRING4 * SLOT;
-  static constexpr int S_BYTES = CW * DP * 4;                 // centre sums [CW][DP] f32 (aliases the ring)
-  static constexpr int OFF_POT = RING;                         // seeding partials [NW][16][64] f32
-  static constexpr int OFF_IAC = OFF_POT + NW * 16 * 64 * 4;   // inertia partials [NW][NCH][64] f32
-  static constexpr int OFF_PRE = OFF_IAC + NW * NCH * 64 * 4;  // closest distances [NW][3][4][64] f32
-  static constexpr int POT_END = OFF_PRE + NW * 3 * 4 * 64 * 4;
-  static constexpr int U_END = POT_END > S_BYTES ? POT_END : S_BYTES;
-  static constexpr int OFF_LW = (U_END + 15) / 16 * 16;       // labels [NW][2][NCH][RT] u8
-  static constexpr int OFF_XN = OFF_LW + NW * 2 * NCH * RT;   // row norms [NRING4][64] f32
-  static constexpr int OFF_ST = OFF_XN + NRING4 * 64 * 4;
-  static constexpr int TOTAL = OFF_ST + ((sizeof(State4) + 15) / 16) * 16;
-  static_assert(TOTAL <= 163840, "LDS budget");
-};
-
-// Thread 0: admit waiting problems into free seeding slots, then pack the next sweep into the 64
-// chunks: seeding problems first (they are on every problem's critical path; one problem per
-// chunk, chunks taken from the top of the emptiest wave), then Lloyd problems round-robin from
-// S.rr, each into the wave with the most free chunks.
-__device__ void schedule4(const KArgs& a, State4& S, const int32_t* idx) {
-  const int P = S.P;
-  for (int p = 0; p < P && S.seedfree; ++p) {
-    if (S.st[p] != ST_WAIT) continue;
-    const int s = __ffs(S.seedfree) - 1;
-    S.seedfree &= ~(1u << s);
-    S.sslot[p] = static_cast<unsigned char>(s);
-    S.st[p] = ST_SEED;
-    S.c[p] = 0;
-  }
-  int lo[NW], hi[NW];  // chunks [0, lo) hold Lloyd problems, [hi, NCH) seeding chunks
-  unsigned wm[NW];
-  for (int w = 0; w < NW; ++w) {
-    lo[w] = 0;
-    hi[w] = NCH;
-    wm[w] = 0;
-    for (int c = 0; c < NCH; ++c) S.cword[w][c] = 0;
-  }
-  for (int s = 0; s < CW; ++s) {
-    S.sitem[s] = -1;
-    S.scl[s] = -1;
-    S.send[s] = 0;
-    S.srow[s] = INT_MIN;
-  }
-  int ni = 0;
-  unsigned long long nseed = 0, nlloyd = 0, nm = 0;
-  // Dense packing: the chunk demand of the sweep decides how many waves are active (an idle
-  // wave skips its distances, E- and M-step); items go worst-fit among the active waves, and a
-  // further wave is opened only when an item fits none of them.
-  int demand = 0;
-  for (int p = 0; p < P; ++p) {
-    if (S.st[p] == ST_SEED) demand += ((S.c[p] == 0 ? 1 : S.ntr[p]) + 3) / 4;
-    else if (S.st[p] == ST_RUN || S.st[p] == ST_FINAL) demand += (S.K[p] + 3) / 4;
-  }
-  int A = min(NW, max(1, (demand + NCH - 1) / NCH));
-  auto pick = [&](int nch) {
-    int w = -1;
-    for (int q = 0; q < A; ++q)
-      if (hi[q] - lo[q] >= nch && (w < 0 || hi[q] - lo[q] > hi[w] - lo[w])) w = q;
-    while (w < 0 && A < NW) {
-      ++A;
-      if (hi[A - 1] - lo[A - 1] >= nch) w = A - 1;
-    }
-    return w;
-  };
-  for (int p = 0; p < P; ++p) S.pitem[p] = -1;
-  for (int p = 0; p < P; ++p) {
-    if (S.st[p] != ST_SEED) continue;
-    const int c = S.c[p];
-    const int nt = (c == 0) ? 1 : S.ntr[p];
-    const int nch = (nt + 3) / 4;
-    if (ni + nt > IMAX) continue;
-    const int w = pick(nch);
-    if (w < 0) continue;
-    S.pitem[p] = static_cast<short>(ni);
-    const int kind = (c == 0) ? IK_SEED0 : IK_SEED;
-    const int cs = (kind == IK_SEED0) ? 0 : S.cs[p];
-    for (int k = 0; k < nch; ++k) {
-      const int ch = hi[w] - nch + k;
-      const int t0 = 4 * k, ncol = min(4, nt - t0);
-      wm[w] |= 1u << (24 + ch);
-      S.cword[w][ch] = static_cast<unsigned>(S.sslot[p]) | (static_cast<unsigned>(cs) << 5) |
-                       (static_cast<unsigned>(t0) << 8) | (static_cast<unsigned>(ncol) << 11) |
-                       (static_cast<unsigned>(kind == IK_SEED) << 14) |
-                       (static_cast<unsigned>(ni + t0) << 16);
-      for (int j = 0; j < ncol; ++j) {
-        const int t = t0 + j, sl = 32 * w + 4 * ch + j;
-        S.ikind[ni + t] = static_cast<unsigned char>(kind);
-        S.iprob[ni + t] = static_cast<unsigned char>(p);
-        S.ioff[ni + t] = static_cast<short>(sl);
-        S.incol[ni + t] = 1;
-        S.itr[ni + t] = static_cast<unsigned char>(t);
-        const int pos = (c == 0) ? a.kpp_pos[S.kidx[p] * a.n_init + S.init[p]] : S.cand[p][t];
-        S.sitem[sl] = static_cast<short>(ni + t);
-        S.srow[sl] = idx[pos];
-      }
-    }
-    hi[w] -= nch;
-    ni += nt;
-    nseed += static_cast<unsigned long long>(nt) * a.m;
-  }
-  int first_skip = -1, last = -1;
-  for (int j = 0; j < P; ++j) {
-    const int p = (S.rr + j) % P;
-    const int st = S.st[p];
-    if (st != ST_RUN && st != ST_FINAL) continue;
-    const int K = S.K[p], nch = (K + 3) / 4;
-    const int w = (ni + 1 <= IMAX) ? pick(nch) : -1;
-    if (w < 0) {
-      if (first_skip < 0) first_skip = p;
-      continue;
-    }
-    const int c0 = lo[w], c1 = c0 + nch - 1;
-    const int kind = (st == ST_RUN) ? IK_RUN : IK_FINAL;
-    S.pitem[p] = static_cast<short>(ni);
-    S.ikind[ni] = static_cast<unsigned char>(kind);
-    S.iprob[ni] = static_cast<unsigned char>(p);
-    S.ioff[ni] = static_cast<short>(32 * w + 4 * c0);
-    S.incol[ni] = static_cast<short>(K);
-    S.itr[ni] = 0;
-    for (int ch = c0; ch <= c1; ++ch) wm[w] |= 1u << ch;
-    wm[w] |= (1u << (8 + c0)) | (1u << (16 + c1));
-    S.cword[w][c1] = static_cast<unsigned>(p) | (static_cast<unsigned>(4 * c0) << 8) |
-                     (static_cast<unsigned>(ni) << 16);
-    for (int k = 0; k < 4 * nch; ++k) {
-      const int sl = 32 * w + 4 * c0 + k;
-      S.send[sl] = static_cast<unsigned char>(c1);
-      if (k < K) {
-        S.sitem[sl] = static_cast<short>(ni);
-        S.scl[sl] = static_cast<short>(st == ST_RUN ? k : -1);
-        S.srow[sl] = -(S.cenoff[p] + k) - 1;
-      }
-    }
-    lo[w] += nch;
-    ++ni;
-    last = p;
-    nlloyd += static_cast<unsigned long long>(K) * a.m;
-    if (st == ST_RUN) nm += a.m;
-  }
-  S.rr = (first_skip >= 0) ? first_skip : (last >= 0 ? (last + 1) % P : S.rr);
-  int active = 0;
-  for (int w = 0; w < NW; ++w) {
-    S.wmask[w] = wm[w];
-    active += (wm[w] != 0);
-  }
-  S.nitems = ni;
-  S.ncols = CW;
-  S.n_seed += nseed;
-  S.n_lloyd += nlloyd;
-  S.n_mrows += nm;
-  if (ni > 0) {
-    S.n_sweeps += 1;
-    S.n_ctiles += static_cast<unsigned long long>(active) * a.T;
-  }
-}
-
-// Per-wave sweep context (wave-uniform words in SGPRs, per-lane values in VGPRs).
-struct Wave4 {
-  unsigned lin, lstart, lend, smask;
-  unsigned cw[NCH];
-};
-
-// E-step of tile te for this wave: Lloyd argmins into the wave's label buffer lw (and the inertia
-// partials of the problems' end chunks), seeding distances into the closest buffers (and the
-// potential partials of the columns).
-template <int DP>
-__device__ __forceinline__ void estep4(const KArgs& a, const Wave4& W, int te, int lane, const v16f& acc,
-                                       const float* cnw, float xn, uint8_t* lw, float* dbuf, int T1,
-                                       const float* pre, float* iac, float* pot) {
-  int ln = lane;
-  asm volatile("" : "+v"(ln));  // per-lane constants recomputed per tile rather than held
-  const int r = ln & 31, hh = ln >> 5;
-  const int erow = te * RT + r;
-  const bool eok = erow < a.m;
-  float bm = 0.f;  // running (min, slot) of the Lloyd problem being merged, in chunk order
-  int bi = 0;
-  // One register group (4 distances, this lane's chunk 2g + hh) at a time: its chunk argmin is
-  // swapped with the other half's, then chunks 2g and 2g + 1 enter the merge in slot order.
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const unsigned gl = (W.lin >> (2 * g)) & 3u, gs = (W.smask >> (2 * g)) & 3u;
-    if ((gl | gs) == 0) continue;  // wave-uniform
-    float d[4];
-    {
-      const float4 c4 = *reinterpret_cast<const float4*>(cnw + 8 * g + 4 * hh);
-      d[0] = c4.x - a.dscale * acc[4 * g];
-      d[1] = c4.y - a.dscale * acc[4 * g + 1];
-      d[2] = c4.z - a.dscale * acc[4 * g + 2];
-      d[3] = c4.w - a.dscale * acc[4 * g + 3];
-    }
-    if (gl) {
-      float m = d[0];
-      int j = 0;
-#pragma unroll
-      for (int q = 1; q < 4; ++q)
-        if (d[q] < m) {
-          m = d[q];
-          j = q;
-        }
-      const int i = 8 * g + 4 * hh + j;
-      const auto bs = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
-      const auto is = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(i), static_cast<unsigned>(i), false, false);
-      const float om = __uint_as_float(hh ? bs[0] : bs[1]);
-      const int oi = static_cast<int>(hh ? is[0] : is[1]);
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {  // chunk 2g (half 0's), then 2g + 1 (half 1's)
-        const int c = 2 * g + e;
-        if (!((W.lin >> c) & 1u)) continue;
-        const float mc = (hh == e) ? m : om;
-        const int ic = (hh == e) ? i : oi;
-        if ((W.lstart >> c) & 1u) {
-          bm = mc;
-          bi = ic;
-        } else if (mc < bm) {
-          bm = mc;
-          bi = ic;
-        }
-        if ((W.lend >> c) & 1u) {
-          const int lab = bi - static_cast<int>((W.cw[c] >> 8) & 0xFFu);
-          if (hh == 0) {
-            lw[c * RT + r] = eok ? static_cast<uint8_t>(lab) : static_cast<uint8_t>(0xFF);
-            if (eok) iac[c * 64] += xn + bm;
-          }
-        }
-      }
-    }
-    if (gs) {
-      const bool mine = (W.smask >> (2 * g + hh)) & 1u;
-      unsigned w = hh ? W.cw[2 * g + 1] : W.cw[2 * g];
-      asm volatile("" : "+v"(w));  // recompute the column addresses per tile rather than hold 16
-      if (mine && eok) {
-        const int sslot = w & 31, cs = (w >> 5) & 7, t0 = (w >> 8) & 7, ncol = (w >> 11) & 7;
-        const bool seed = (w >> 14) & 1u;
-        const float cl = pre[g * 64];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (j >= ncol) break;
-          const float dist = fmaxf(xn + d[j], 0.f);
-          const float dm = seed ? fminf(cl, dist) : dist;
-          const int t = t0 + j;
-          const int ws = seed ? ((t < cs) ? t : t + 1) : 0;
-          dbuf[(static_cast<size_t>(sslot) * T1 + ws) * a.lsm + erow] = dm;
-          pot[(4 * g + j) * 64] += dm;
-        }
-      }
-    }
-  }
-}
-
-// Closest distances of this lane's seeding chunks for tile tp, loaded by LDS-DMA into the wave's
-// buffer dst[g * 64 + lane] (one global_load_lds_dword per seeding register group; lanes with
-// nothing to load fetch a harmless dummy word).  Completion: the end-of-tile DMA wait.
-__device__ __forceinline__ void prefetch4(const KArgs& a, const Wave4& W, int tp, int lane, const float* dbuf,
-                                          int T1, float* dst) {
-  const int hh = lane >> 5;
-  const int row = tp * RT + (lane & 31);
-  const bool ok = tp < a.T && row < a.m;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    if (((W.smask >> (2 * g)) & 3u) == 0) continue;  // wave-uniform
-    const bool mine = (W.smask >> (2 * g + hh)) & 1u;
-    unsigned w = hh ? W.cw[2 * g + 1] : W.cw[2 * g];
-    asm volatile("" : "+v"(w));
-    const bool load = mine && ok && ((w >> 14) & 1u);
-    const float* src = load ? dbuf + (static_cast<size_t>(w & 31) * T1 + ((w >> 5) & 7)) * a.lsm + row : dbuf;
-    dma_piece(src, dst + g * 64, 4);
-  }
-}
-
-// Add the f32 partials into the items' f64 accumulators (one contributing half per item: half 0
-// for Lloyd problems, the chunk's half for seeding columns) and restart them.
-__device__ __forceinline__ void flush4(State4& S, const Wave4& W, int lane, float* iac, float* pot) {
-  const int r = lane & 31, hh = lane >> 5;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    if (!((W.lend >> c) & 1u)) continue;
-    const double v = half_sum(static_cast<double>(iac[c * 64]));
-    if (r == 0 && hh == 0) S.iinert[(W.cw[c] >> 16) & 0xFF] += v;
-    iac[c * 64] = 0.f;
-  }
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    if (((W.smask >> (2 * g)) & 3u) == 0) continue;
-    const bool mine = (W.smask >> (2 * g + hh)) & 1u;
-    const unsigned w = hh ? W.cw[2 * g + 1] : W.cw[2 * g];
-    const int ncol = (w >> 11) & 7, item0 = (w >> 16) & 0xFF;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const double v = half_sum(static_cast<double>(pot[(4 * g + j) * 64]));
-      if (mine && r == 0 && j < ncol) S.iinert[item0 + j] += v;
-      pot[(4 * g + j) * 64] = 0.f;
-    }
-  }
-}
-
-template <int DP>
-__global__ __launch_bounds__(NT, 1) void kmeans4_kernel(KArgs a) {
-  using LY = Lay4<DP>;
-  __shared__ __attribute__((aligned(16))) char smem[LY::TOTAL];
-  char* ring = smem;
-  float* Sm = reinterpret_cast<float*>(smem);  // [CW][DP] sums (aliases the ring)
-  uint8_t* Lw = reinterpret_cast<uint8_t*>(smem + LY::OFF_LW);
-  float* XN = reinterpret_cast<float*>(smem + LY::OFF_XN);
-  State4& S = *reinterpret_cast<State4*>(smem + LY::OFF_ST);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int m = a.m, T = a.T;
-  uint8_t* wsb = a.ws + static_cast<size_t>(blockIdx.x) * a.ws_per_wg;
-  uint8_t* glab = wsb;                                                  // [Pws][lsm] (one buffer each)
-  float* cen = reinterpret_cast<float*>(wsb + a.off_cen);               // [Cws][DP]
-  float* cenn = reinterpret_cast<float*>(wsb + a.off_cenn);             // [Cws]
-  int32_t* cpos = reinterpret_cast<int32_t*>(wsb + a.off_cpos);         // [Pws][Kws]
-  float* dbuf = reinterpret_cast<float*>(wsb + a.off_dbuf);             // [seedmax][Tws+1][m]
-  float* rdist = reinterpret_cast<float*>(wsb + a.off_rdist);           // [m]
-  const int T1 = a.Tws + 1;
-  uint8_t* lwave = Lw + wave * (2 * NCH * RT);
-  if (tid == 0) S.n_lloyd = S.n_seed = S.n_mrows = S.n_reloc = S.n_sweeps = S.n_ctiles = 0;
-
-  for (;;) {
-    __syncthreads();
-    if (tid == 0) S.unit = static_cast<int>(atomicAdd(a.counter, 1u));
-    __syncthreads();
-    const int unit = S.unit;
-    if (unit >= a.nh * a.nU) break;
-    const int hb = unit / a.nU, g = unit - hb * a.nU;
-    const int h = a.h_begin + hb;
-    const int32_t* idx = a.idx + static_cast<size_t>(h) * m;
-    const int32_t* gd = a.units + g * US;
-
-    if (tid == 0) {
-      const int P = gd[0];
-      S.P = P;
-      int o = 0;
-      for (int p = 0; p < P; ++p) {
-        S.K[p] = static_cast<unsigned char>(gd[1 + 4 * p]);
-        S.kidx[p] = static_cast<unsigned char>(gd[2 + 4 * p]);
-        S.init[p] = static_cast<unsigned char>(gd[3 + 4 * p]);
-        S.ntr[p] = static_cast<unsigned char>(gd[4 + 4 * p]);
-        S.st[p] = ST_WAIT;
-        S.iter[p] = 0;
-        S.cenoff[p] = static_cast<short>(o);
-        o += S.K[p];
-      }
-      S.rr = 0;
-      S.seedfree = (a.seedmax >= 32) ? 0xFFFFFFFFu : ((1u << a.seedmax) - 1u);
-    }
-    __syncthreads();
-    const int P = S.P;
-    for (size_t e = tid; e < static_cast<size_t>(P) * a.lsm; e += NT) glab[e] = 0xFF;
-
-    // ---- tol = tol_rel * mean(var(X_sub, axis=0)) (sklearn _tolerance, :270-278) --
-    {
-      double* red = reinterpret_cast<double*>(ring);  // [NT/DP][DP]
-      double* mean = reinterpret_cast<double*>(ring) + NT;
-      constexpr int NPH = NT / DP;
-      const int d = tid % DP, ph = tid / DP;
-      double s = 0.0;
-      for (int r = ph; r < m; r += NPH) s += static_cast<double>(a.X[static_cast<size_t>(idx[r]) * DP + d]);
-      red[ph * DP + d] = s;
-      __syncthreads();
-      if (tid < DP) {
-        double t = 0.0;
-        for (int k = 0; k < NPH; ++k) t += red[k * DP + tid];
-        mean[tid] = t / m;
-      }
-      __syncthreads();
-      const double mu = mean[d];
-      double q = 0.0;
-      for (int r = ph; r < m; r += NPH) {
-        const double v = static_cast<double>(a.X[static_cast<size_t>(idx[r]) * DP + d]) - mu;
-        q += v * v;
-      }
-      __syncthreads();
-      red[ph * DP + d] = q;
-      __syncthreads();
-      if (tid == 0) {
-        double tot = 0.0;
-        for (int dd = 0; dd < a.dreal; ++dd) {
-          double t = 0.0;
-          for (int k = 0; k < NPH; ++k) t += red[k * DP + dd];
-          tot += t / m;
-        }
-        S.tol = static_cast<float>(static_cast<float>(tot / a.dreal) * a.tol_rel);
-      }
-      __syncthreads();
-    }
-
-    // ---- sweeps -----------------------------------------------------------------
-    for (;;) {
-      if (tid == 0) schedule4(a, S, idx);
-      __syncthreads();
-      const int nitems = S.nitems, ncols = S.ncols;
-      if (nitems == 0) break;
-      if (tid < ncols) {
-        const int sr = S.srow[tid];
-        S.cnorm[tid] = (sr >= 0) ? a.xnorm[sr] : (sr == INT_MIN ? __builtin_huge_valf() : cenn[-sr - 1]);
-      }
-      if (tid < IMAX) S.iinert[tid] = 0.0;
-      Wave4 W;
-      {
-        const unsigned wm = __builtin_amdgcn_readfirstlane(S.wmask[wave]);
-        W.lin = wm & 0xFFu;
-        W.lstart = (wm >> 8) & 0xFFu;
-        W.lend = (wm >> 16) & 0xFFu;
-        W.smask = wm >> 24;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) W.cw[c] = __builtin_amdgcn_readfirstlane(S.cword[wave][c]);
-      }
-      const bool tact = (W.lin | W.smask) != 0;  // wave-uniform
-      const int hh = lane >> 5, lr = lane & 31;
-      const int sl = 32 * wave + lr;
-      h8 ah[DP / 16], al[DP / 16];
-      {
-        const int sr = S.srow[sl];
-        const bool ok = sr != INT_MIN;
-        const float* src = (sr >= 0) ? a.X + static_cast<size_t>(sr) * DP
-                                     : cen + static_cast<size_t>(ok ? -sr - 1 : 0) * DP;
-        afrag_load<DP>(ah, al, src, ok, hh, a.scale);
-      }
-      v16f sacc[DP / 32];
-#pragma unroll
-      for (int dt = 0; dt < DP / 32; ++dt) sacc[dt] = v16f{};
-      unsigned mcnt = 0;
-      const int mycl = S.scl[sl];
-      const int myend = S.send[sl];
-      const bool mact = __ballot(mycl >= 0) != 0ull;  // wave-uniform: any running centre
-      // label store lanes: chunk lane >> 3, rows 4 (lane & 7) .. +3
-      const int lcq = lane >> 3, lrq = 4 * (lane & 7);
-      const bool lst = (W.lend >> lcq) & 1u;
-      const int lp = static_cast<int>(S.cword[wave][lcq] & 0x3Fu);
-      uint8_t* lgl = glab + static_cast<size_t>(lst ? lp : 0) * a.lsm + lrq;
-      bool chg = false;
-      float* pot = reinterpret_cast<float*>(smem + LY::OFF_POT) + wave * (16 * 64) + lane;
-      float* iac = reinterpret_cast<float*>(smem + LY::OFF_IAC) + wave * (NCH * 64) + lane;
-      float* prebuf = reinterpret_cast<float*>(smem + LY::OFF_PRE) + wave * (3 * 4 * 64);  // [3][4][64]
-#pragma unroll
-      for (int v = 0; v < 16; ++v) pot[v * 64] = 0.f;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) iac[c * 64] = 0.f;
-      // pipeline prologue: tile 0 in the ring, indices of tile 1; operands of tile 0
-      TileIdx<DP> nI;
-      {
-        TileIdx<DP> I0;
-        idx_issue<DP>(a, idx, 0, wave, lane, I0);
-        tile_dma<DP>(a, I0, ring, XN, wave, lane);
-        idx_issue<DP>(a, idx, RT, wave, lane, nI);
-        prefetch4(a, W, 0, lane, dbuf, T1, prebuf);
-        dma_wait();
-      }
-      unsigned lold = lst ? *reinterpret_cast<const unsigned*>(lgl) : 0u;
-      __syncthreads();  // cnorm, iinert, tile 0
-      const float* cnw = S.cnorm + 32 * wave;
-#ifdef CC_KM_STAMPS
-      unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-      // distances of tile t (the v3 MFMA sequence) into acc
-      auto dist = [&](int t, v16f& acc) __attribute__((always_inline)) {
-        const char* xs = ring + (t % NRING4) * LY::SLOT;
-        acc = v16f{};
-        int lro = lr;
-        asm volatile("" : "+v"(lro));
-        h8 bh = *reinterpret_cast<const h8*>(xs + xoff<DP>(lro, hh));
-        h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + xoff<DP>(lro, hh));
-#pragma unroll
-        for (int s = 0; s < DP / 16; ++s) {
-          h8 nh = bh, nl = bl;
-          if (s + 1 < DP / 16) {
-            const int off = xoff<DP>(lro, 2 * (s + 1) + hh);
-            nh = *reinterpret_cast<const h8*>(xs + off);
-            nl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
-          }
-          acc = mfma16(ah[s], bl, acc);
-          acc = mfma16(al[s], bh, acc);
-          acc = mfma16(ah[s], bh, acc);
-          __builtin_amdgcn_sched_barrier(0);
-          bh = nh;
-          bl = nl;
-        }
-      };
-      // E-step of tile te from acc
-      auto estep_of = [&](int te, const v16f& acc) __attribute__((always_inline)) {
-        const float xn = XN[(te % NRING4) * 64 + lr];
-        estep4<DP>(a, W, te, lane, acc, cnw, xn, lwave + (te & 1) * (NCH * RT), dbuf, T1,
-                   prebuf + (te % 3) * (4 * 64) + lane, iac, pot);
-        __builtin_amdgcn_wave_barrier();
-      };
-      // M-step of tile tm (one-hot x X on f16 MFMA; counts by popcount), its label store (old
-      // label word lo) and the flush of the partials
-      auto mstep = [&](int tm, unsigned lo) __attribute__((always_inline)) {
-        const char* xs = ring + (tm % NRING4) * LY::SLOT;
-        const uint8_t* lw = lwave + (tm & 1) * (NCH * RT);
-        if (mact) {
-          const uint8_t* lsb = lw + myend * RT;
-          int ln = lane;
-          asm volatile("" : "+v"(ln));  // recompute the transposed-read offsets per tile
-          const int G = ln >> 4, q = (ln >> 2) & 3, pp = ln & 3;
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const unsigned long long lab8 = *reinterpret_cast<const unsigned long long*>(lsb + 16 * s2 + 8 * hh);
-            u32x4 ohu;
-            unsigned nb = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
-              const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
-              ohu[j] = ((b0 == mycl) ? 0x3C00u : 0u) | ((b1 == mycl) ? 0x3C000000u : 0u);
-              nb += (b0 == mycl) + (b1 == mycl);
-            }
-            mcnt += nb;
-            const h8 oh = __builtin_bit_cast(h8, ohu);
-            const int row0 = 16 * s2 + 8 * (G >> 1) + q;
-            auto rd = [&](int dt, s4 (&rr)[4]) __attribute__((always_inline)) {
-              const int chn = 4 * dt + 2 * (G & 1) + (pp >> 1);
-              const int a0 = xoff<DP>(row0, chn) + 8 * (pp & 1);
-              const int a1 = xoff<DP>(row0 + 4, chn) + 8 * (pp & 1);
-              rr[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a0));
-              rr[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a1));
-              rr[2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a0));
-              rr[3] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a1));
-            };
-            s4 rc[4], rn[4];
-            rd(0, rc);
-#pragma unroll
-            for (int dt = 0; dt < DP / 32; ++dt) {
-              if (dt + 1 < DP / 32) rd(dt + 1, rn);
-              const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(rc[0], rc[1], 0, 1, 2, 3, 4, 5, 6, 7));
-              const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(rc[2], rc[3], 0, 1, 2, 3, 4, 5, 6, 7));
-              sacc[dt] = mfma16(oh, bl, sacc[dt]);
-              sacc[dt] = mfma16(oh, bh, sacc[dt]);
-              __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-              for (int k = 0; k < 4; ++k) rc[k] = rn[k];
-            }
-          }
-        }
-        if (lst) {  // labels of tile tm vs the previous sweep's; store (one dword = 4 rows per lane)
-          const unsigned w32 = *reinterpret_cast<const unsigned*>(lw + lcq * RT + lrq);
-          chg |= (w32 != lo);
-          *reinterpret_cast<unsigned*>(lgl + tm * RT) = w32;
-        }
-        if ((tm % FLUSH) == FLUSH - 2) flush4(S, W, lane, iac, pot);  // the v3 flush windows
-      };
-      // gather of tile t+1 (LDS-DMA rows, row norms, closest distances), indices of tile t+2
-      auto issue = [&](int t) __attribute__((always_inline)) {
-        if (t + 1 < T) {
-          tile_dma<DP>(a, nI, ring + ((t + 1) % NRING4) * LY::SLOT, XN + ((t + 1) % NRING4) * 64, wave, lane);
-          prefetch4(a, W, t + 1, lane, dbuf, T1, prebuf + ((t + 1) % 3) * (4 * 64));
-        }
-        if (t + 2 < T) idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
-      };
-      // Waves w and w + 4 share a SIMD.  Waves 0-3 run distances(t) -> E-step(t) -> M-step(t);
-      // waves 4-7 lag one tile, E-step(t-1) -> M-step(t-1) -> distances(t), so that one wave's
-      // E-step vector work overlaps its partner's distance MFMAs.  Every result is the same
-      // either way; the ring keeps tile t-1 until iteration t+1.  Both loops pass T + 1 barriers.
-      if (wave < NW / 2) {
-        for (int t = 0; t <= T; ++t) {
-          KM_STAMP(s0);
-          issue(t);
-          const unsigned nlold = (lst && t + 1 < T) ? *reinterpret_cast<const unsigned*>(lgl + (t + 1) * RT) : 0u;
-          KM_STAMP(s1);
-          if (t < T) {
-            v16f acc;
-            if (tact) dist(t, acc);
-            KM_STAMP(s2);
-            KM_ACC(1, s1, s2);
-            if (tact) estep_of(t, acc);
-            KM_STAMP(s3);
-            KM_ACC(2, s2, s3);
-            mstep(t, lold);
-            KM_STAMP(s4);
-            KM_ACC(3, s3, s4);
-          }
-          lold = nlold;
-          KM_STAMP(s5);
-          dma_wait();
-          __syncthreads();
-          KM_STAMP(s6);
-          KM_ACC(0, s0, s1);
-          KM_ACC(4, s5, s6);
-        }
-      } else {
-        v16f acc = {};
-        unsigned lold1 = 0u;
-        for (int t = 0; t <= T; ++t) {
-          KM_STAMP(s0);
-          issue(t);
-          const unsigned nlold = (lst && t + 1 < T) ? *reinterpret_cast<const unsigned*>(lgl + (t + 1) * RT) : 0u;
-          KM_STAMP(s1);
-          if (t >= 1) {
-            if (tact) estep_of(t - 1, acc);
-            KM_STAMP(s2);
-            KM_ACC(2, s1, s2);
-            mstep(t - 1, lold1);
-            KM_STAMP(s3);
-            KM_ACC(3, s2, s3);
-          }
-          KM_STAMP(s4);
-          if (t < T && tact) dist(t, acc);
-          KM_STAMP(s5);
-          KM_ACC(1, s4, s5);
-          lold1 = lold;
-          lold = nlold;
-          dma_wait();
-          __syncthreads();
-          KM_STAMP(s6);
-          KM_ACC(0, s0, s1);
-          KM_ACC(4, s5, s6);
-        }
-      }
-#ifdef CC_KM_STAMPS
-      if (blockIdx.x == 0 && lane == 0 && a.stats)
-        for (int k = 0; k < 7; ++k) atomicAdd(&a.stats[8 + 8 * wave + k], st_acc[k]);
-#endif
-      flush4(S, W, lane, iac, pot);
-      // labels changed, per Lloyd problem of this wave
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        if (!((W.lend >> c) & 1u)) continue;
-        const bool any = __ballot(chg && lcq == c) != 0ull;
-        if (lane == 0) S.ichanged[(W.cw[c] >> 16) & 0xFF] = any ? 1u : 0u;
-      }
-      // sums -> Sm (aliases the ring: every reader passed the last barrier); counts
-      if (mact) {
-#pragma unroll
-        for (int dt = 0; dt < DP / 32; ++dt)
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int s2 = 32 * wave + (v & 3) + 8 * (v >> 2) + 4 * hh;
-            Sm[s2 * DP + 32 * dt + lr] = sacc[dt][v] * a.inv_scale;
-          }
-        const unsigned tot = mcnt + __shfl_xor(mcnt, 32);
-        if (hh == 0) S.cnt[sl] = tot;
-      }
-      __syncthreads();
-            // ---- seeding decisions (thread per problem) -----------------------------------
-      if (tid < P) {
-        const int p = tid;
-        S.need_sel[p] = 0;
-        S.to_run[p] = 0;
-        if (S.st[p] == ST_SEED && S.pitem[p] >= 0) {
-          const int it0 = S.pitem[p], c = S.c[p];
-          const int nt = (c == 0) ? 1 : S.ntr[p];
-          int best = 0;
-          float bv = static_cast<float>(S.iinert[it0]);
-          for (int t = 1; t < nt; ++t) {
-            const float v = static_cast<float>(S.iinert[it0 + t]);
-            if (v < bv) {
-              bv = v;
-              best = t;
-            }
-          }
-          S.pot32[p] = bv;
-          const int cs = S.cs[p];
-          S.cs[p] = static_cast<unsigned char>((c == 0) ? 0 : ((best < cs) ? best : best + 1));
-          S.sbest[p] = static_cast<unsigned char>(best);
-          cpos[p * a.Kws + c] = (c == 0) ? a.kpp_pos[S.kidx[p] * a.n_init + S.init[p]] : S.cand[p][best];
-          S.c[p] = static_cast<unsigned char>(c + 1);
-          if (c + 1 == S.K[p]) {
-            S.to_run[p] = 1;  // seeding slot released below (single writer)
-          } else {
-            S.need_sel[p] = 1;
-          }
-        }
-      }
-      __syncthreads();
-      if (tid == 0) {
-        for (int p = 0; p < P; ++p)
-          if (S.to_run[p]) {
-            S.seedfree |= 1u << S.sslot[p];
-            S.st[p] = ST_RUN;
-            S.iter[p] = 0;
-          }
-      }
-      // candidate selection: one wave per problem
-      {
-        int j = 0;
-        for (int p = 0; p < P; ++p) {
-          if (!S.need_sel[p]) continue;
-          if ((j++ % NW) != wave) continue;
-          const int ss = S.sslot[p];
-          kpp_select(a, S, p, dbuf + (static_cast<size_t>(ss) * T1 + S.cs[p]) * a.lsm, lane);
-        }
-      }
-      // initial centres of problems leaving seeding: the chosen rows (exact f32)
-      for (int p = 0; p < P; ++p) {
-        if (!S.to_run[p]) continue;
-        const int K = S.K[p];
-        for (int e = tid; e < K * DP; e += NT) {
-          const int c = e / DP, d = e - c * DP;
-          cen[(S.cenoff[p] + c) * DP + d] = a.X[static_cast<size_t>(idx[cpos[p * a.Kws + c]]) * DP + d];
-        }
-        if (tid < K) cenn[S.cenoff[p] + tid] = row_sq(a.X + static_cast<size_t>(idx[cpos[p * a.Kws + tid]]) * DP, a.dreal);
-      }
-
-      // ---- Lloyd M-step completion (RUN items) ------------------------------------
-      if (tid == 0) {
-        int f = 0;
-        for (int it = 0; it < nitems; ++it) {
-          if (S.ikind[it] != IK_RUN) continue;
-          const int p = S.iprob[it], off = S.ioff[it];
-          int ne = 0;
-          for (int c = 0; c < S.K[p]; ++c) ne += (S.cnt[off + c] == 0);
-          S.nempty[p] = ne;
-          f |= (ne > 0);
-        }
-        S.flag = f;
-      }
-      __syncthreads();
-      if (S.flag) {
-        for (int it = 0; it < nitems; ++it) {
-          if (S.ikind[it] != IK_RUN) continue;
-          const int p = S.iprob[it];
-          if (S.nempty[p] == 0) continue;
-          relocate<DP>(a, idx, p, S.ioff[it], cen, Sm, S, glab + static_cast<size_t>(p) * a.lsm,
-                       rdist, tid);
-          __syncthreads();
-        }
-      }
-      // first argmax of counts per problem (for clusters still empty: _average_centers)
-      if (tid < nitems && S.ikind[tid] == IK_RUN) {
-        const int p = S.iprob[tid], off = S.ioff[tid];
-        int am = 0;
-        for (int c = 1; c < S.K[p]; ++c)
-          if (S.cnt[off + c] > S.cnt[off + am]) am = c;
-        S.amax[p] = am;
-      }
-      __syncthreads();
-      // _average_centers (_k_means_common.pyx:215-237) runs j in order: an empty cluster
-      // j copies centre argmax(weight), which is still a raw sum when j < argmax.
-      for (int e = tid; e < ncols * DP; e += NT) {
-        const int sl = e / DP, d = e - sl * DP;
-        const int it = S.sitem[sl];
-        if (it < 0 || S.ikind[it] != IK_RUN || S.cnt[sl] != 0) continue;
-        const int p = S.iprob[it], off = S.ioff[it];
-        if (sl - off > S.amax[p]) continue;
-        Sm[sl * DP + d] = Sm[(off + S.amax[p]) * DP + d];
-      }
-      __syncthreads();
-      for (int e = tid; e < ncols * DP; e += NT) {
-        const int sl = e / DP;
-        if (S.sitem[sl] < 0 || S.ikind[S.sitem[sl]] != IK_RUN) continue;
-        const unsigned cn = S.cnt[sl];
-        if (cn > 0) {
-          const float alpha = static_cast<float>(1.0 / static_cast<double>(static_cast<float>(cn)));
-          Sm[e] *= alpha;
-        }
-      }
-      __syncthreads();
-      for (int e = tid; e < ncols * DP; e += NT) {
-        const int sl = e / DP, d = e - sl * DP;
-        const int it = S.sitem[sl];
-        if (it < 0 || S.ikind[it] != IK_RUN || S.cnt[sl] != 0) continue;
-        const int p = S.iprob[it], off = S.ioff[it];
-        if (sl - off < S.amax[p]) continue;
-        Sm[sl * DP + d] = Sm[(off + S.amax[p]) * DP + d];
-      }
-      __syncthreads();
-      // centre shifts (sklearn _euclidean_dense_dense, 4-way unrolled f32)
-      if (tid < ncols && S.sitem[tid] >= 0 && S.ikind[S.sitem[tid]] == IK_RUN) {
-        const int sl = tid;
-        const int it = S.sitem[sl];
-        const int p = S.iprob[it];
-        const float* cnw = Sm + sl * DP;
-        const float* co = cen + (S.cenoff[p] + (sl - S.ioff[it])) * DP;
-        float res = 0.f;
-        const int n4 = a.dreal / 4, rem = a.dreal % 4;
-        for (int i = 0; i < n4; ++i) {
-          const float d0 = cnw[4 * i] - co[4 * i], d1 = cnw[4 * i + 1] - co[4 * i + 1];
-          const float d2 = cnw[4 * i + 2] - co[4 * i + 2], d3 = cnw[4 * i + 3] - co[4 * i + 3];
-          res += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
-        }
-        for (int i = 0; i < rem; ++i) {
-          const float dd = cnw[4 * n4 + i] - co[4 * n4 + i];
-          res += dd * dd;
-        }
-        const float sh = sqrtf(res);
-        S.shift[sl] = sh * sh;
-      }
-      __syncthreads();
-      // convergence decisions (_kmeans_single_lloyd :697-736)
-      if (tid < nitems && S.ikind[tid] >= IK_RUN) {
-        const int it = tid, p = S.iprob[it];
-        if (S.ikind[it] == IK_RUN) {
-          S.iter[p] += 1;
-          if (!S.ichanged[it]) {
-            S.st[p] = ST_DONE;  // strict convergence: final labels are this sweep's
-            S.inert[p] = static_cast<float>(S.iinert[it]);
-          } else {
-            const float tot = np_pairwise_sum(S.shift + S.ioff[it], S.K[p]);
-            S.st[p] = (tot <= S.tol || S.iter[p] >= a.max_iter) ? ST_FINAL : ST_RUN;
-          }
-        } else {
-          S.st[p] = ST_DONE;
-          S.inert[p] = static_cast<float>(S.iinert[it]);
-        }
-      }
-      __syncthreads();
-      // write back the centres (and norms) of problems that sweep again
-      for (int e = tid; e < ncols * DP; e += NT) {
-        const int sl = e / DP, d = e - sl * DP;
-        const int it = S.sitem[sl];
-        if (it < 0 || S.ikind[it] != IK_RUN) continue;
-        const int p = S.iprob[it];
-        if (S.st[p] == ST_DONE) continue;
-        cen[(S.cenoff[p] + (sl - S.ioff[it])) * DP + d] = Sm[e];
-      }
-      if (tid < ncols) {
-        const int it = S.sitem[tid];
-        if (it >= 0 && S.ikind[it] == IK_RUN) {
-          const int p = S.iprob[it];
-          if (S.st[p] != ST_DONE) cenn[S.cenoff[p] + (tid - S.ioff[it])] = row_sq(Sm + tid * DP, a.dreal);
-        }
-      }
-      __syncthreads();
-    }
-
-    // ---- best of n_init per K, output (KMeans.fit :1495-1531) -------------------
-    for (int p0 = 0; p0 < P; p0 += a.n_init) {
-      int best = p0;
-      for (int i = 1; i < a.n_init; ++i) {
-        const int p = p0 + i;
-        if (!(S.inert[p] < S.inert[best])) continue;
-        // _is_same_clustering(labels_p, labels_best): labels_p -> labels_best must be a function
-        if (tid <= KMAX) S.map[tid] = -1;
-        if (tid == 0) S.flag = 0;
-        __syncthreads();
-        const uint8_t* l1 = glab + static_cast<size_t>(p) * a.lsm;
-        const uint8_t* l2 = glab + static_cast<size_t>(best) * a.lsm;
-        for (int r = tid; r < m; r += NT) S.map[l1[r]] = l2[r];
-        __syncthreads();
-        bool bad = false;
-        for (int r = tid; r < m; r += NT) bad |= (S.map[l1[r]] != l2[r]);
-        if (bad) S.flag = 1;
-        __syncthreads();
-        if (S.flag) best = p;
-        __syncthreads();
-      }
-      const int kidx = S.kidx[p0];
-      const uint8_t* lb = glab + static_cast<size_t>(best) * a.lsm;
-      uint8_t* out = a.labels_out + static_cast<size_t>(kidx) * a.n * a.ldl + h;
-      for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = lb[r];
-      if (tid == 0) {
-        if (a.inertia_out) a.inertia_out[static_cast<size_t>(kidx) * a.H + h] = S.inert[best];
-        if (a.niter_out) a.niter_out[static_cast<size_t>(kidx) * a.H + h] = S.iter[best];
-      }
-    }
-  }
-  if (tid == 0 && a.stats) {
-    atomicAdd(&a.stats[0], S.n_lloyd);
-    atomicAdd(&a.stats[1], S.n_seed);
-    atomicAdd(&a.stats[2], S.n_mrows);
-    atomicAdd(&a.stats[3], S.n_reloc);
-    atomicAdd(&a.stats[4], S.n_sweeps);
-    atomicAdd(&a.stats[5], S.n_ctiles);
-  }
-}
-
 // f16 hi/lo image of the rows: Xhl[r][0][d] = f16(x s), Xhl[r][1][d] = f16(x s - hi), s = 2^e.
 __global__ void split_kernel(const float* X, long long total, int dpad, float scale, uint16_t* Xhl) {
   const long long i = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -2355,9 +1433,8 @@ WsLayout ws_layout(int m, int dpad, const int32_t* units, int nU, int seedmax) {
 }
 
 template <int DP>
-void launch(const KArgs& a, unsigned blocks, hipStream_t st, bool v4) {
-  if (v4) hipLaunchKernelGGL(kmeans4_kernel<DP>, dim3(blocks), dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL(kmeans_kernel<DP>, dim3(blocks), dim3(NT), 0, st, a);
+void launch(const KArgs& a, unsigned blocks, hipStream_t st) {
+  hipLaunchKernelGGL(kmeans_kernel<DP>, dim3(blocks), dim3(NT), 0, st, a);
 }
 
 }  // namespace
@@ -2544,15 +1621,10 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
   a.seedmax = seedmax;
   a.lsm = (m + 63) & ~63;
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nU));
-  // Engine v3 by default.  CCMI_KM_ENGINE=4 selects v4 (wave-local problems, K <= 32): the two
-  // engines give bit-identical results; v4 measured slower at C3 (3.51 s vs 2.50 s, see
-  // DESIGN.md section 3) and is kept as the tested alternative schedule.
-  const char* eng = std::getenv("CCMI_KM_ENGINE");
-  const bool v4 = kmax <= KMAX4 && eng && eng[0] == '4';
   switch (dpad) {
-    case 32: launch<32>(a, blocks, st, v4); break;
-    case 64: launch<64>(a, blocks, st, v4); break;
-    default: launch<128>(a, blocks, st, v4); break;
+    case 32: launch<32>(a, blocks, st); break;
+    case 64: launch<64>(a, blocks, st); break;
+    default: launch<128>(a, blocks, st); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) {

@@ -240,37 +240,3 @@ def test_f64_labels_match_sklearn_float64(n, d, k_true, Ks, H):
                 assert not np.array_equal(km32.labels_, km.labels_), (K, h, np.mean(km.labels_ == got))
                 ill += 1
     assert exact >= 0.9 * (exact + ill), (exact, ill)
-
-
-@pytest.mark.parametrize("n,d,k_true,Ks,H,std", [
-    (3000, 128, 8, [2, 5, 8, 13, 20], 6, 1.0),
-    (2500, 64, 6, [2, 3, 6, 9, 15, 32], 5, 2.0),
-    (4000, 32, 5, [2, 4, 7, 10], 8, 3.0),
-    (700, 100, 4, [3, 17, 31], 4, 6.0),   # heavy overlap: relocations, long Lloyd runs
-])
-def test_engine_v4_matches_v3(monkeypatch, n, d, k_true, Ks, H, std):
-    """The v4 engine (wave-local problems, in-register E-step) computes the same distances,
-    argmins, f32 partials and flush windows as v3: labels, inertia and iteration counts must
-    be bit-identical, whatever the packing of the sweeps."""
-    dev = engine.require_gpu()
-    X = blobs(n, d, k_true, seed=d + n, std=std)
-    m = int(0.8 * n)
-    idx = engine.resample_indices(5, n, m, 0, H)
-    idx_d = torch.from_numpy(idx).to(dev)
-    Xd, xn, _, Xhl, e = prepare_rows(X, dev)
-    out = []
-    for eng in ("3", "4"):
-        monkeypatch.setenv("CCMI_KM_ENGINE", eng)
-        L = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
-        inert = torch.zeros((len(Ks), H), dtype=torch.float32, device=dev)
-        nit = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
-        bk = BatchedKMeans(Ks, random_state=5)
-        bk.run(Xd, xn, d, idx_d, n, H, m, 0, H, L, np.float32, inertia=inert, n_iter=nit, Xhl=Xhl,
-               scale_exp=e)
-        torch.cuda.synchronize()
-        out.append((L, inert, nit, bk.stats.clone()))
-    (L3, i3, n3, s3), (L4, i4, n4, s4) = out
-    assert torch.equal(L3, L4)
-    assert torch.equal(i3, i4)
-    assert torch.equal(n3, n4)
-    assert int(s3[0]) == int(s4[0]) and int(s3[1]) == int(s4[1])  # same Lloyd / seeding work

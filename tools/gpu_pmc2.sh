@@ -1,17 +1,15 @@
-# SQ counter passes on the k-means launch alone for both engines (v4 default, v3 forced).
-# Usage: bash tools/gpu_pmc2.sh [H]
+# SQ counter passes on the k-means launch alone (tools/km_only.py H), summarised per wave and
+# tile iteration.  Usage: bash tools/gpu_pmc2.sh [H]
 export TMPDIR=/tmp
 H=${1:-64}
-for ENG in 4 3; do
-  OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_e$ENG
-  mkdir -p $OUT
-  P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES"
-  P2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS"
-  P3="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_MISC"
-  i=0
-  for P in "$P1" "$P2" "$P3"; do
-    i=$((i+1))
-    (cd /tmp && CCMI_KM_ENGINE=$ENG timeout -s KILL 120 rocprofv3 --pmc $P -d $OUT/p$i -o p$i --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/km_only.py $H > $OUT/p$i.log 2>&1) || { echo "engine $ENG pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
-  done
-  echo "== engine $ENG"; python3 tools/pmc_summary.py $OUT
+OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_km
+mkdir -p $OUT
+P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES"
+P2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS"
+P3="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_MISC"
+i=0
+for P in "$P1" "$P2" "$P3"; do
+  i=$((i+1))
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $P -d $OUT/p$i -o p$i --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/km_only.py $H > $OUT/p$i.log 2>&1) || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
+python3 tools/pmc_summary.py $OUT

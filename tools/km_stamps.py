@@ -23,8 +23,8 @@ cc.fit(torch.from_numpy(X).cuda())
 st = cc.kmeans_stats_.cpu().numpy()
 print("timings", cc.timings_)
 print("counters lloyd/seed/mrows/reloc/sweeps/ctiles", st[:6])
-# v4 engine: issue, dist, estep, mstep(+labels, flush), wait+barrier; v3 (CCMI_KM_ENGINE=3): issue, dist, estep, mstep, commit, barrier, prologue
-names = ["k0", "k1", "k2", "k3", "k4", "k5", "k6"]
+# phases: issue, dist, estep, mstep, commit, barrier, prologue
+names = ["issue", "est4+dist", "est0-3", "mstep", "wait", "barrier", "prologue"]
 for w in range(8):
     v = st[8 + 8 * w: 15 + 8 * w]
     tot = max(v.sum(), 1)
