@@ -170,13 +170,14 @@ def cpu_baseline(cfg, X, H_sample=8):
     }
 
 
-def load_traffic(config, kernel, prefix="profiles"):
-    """Per-launch HBM bytes of `kernel` at `config` from a committed PMC summary
-    (profiles/traffic/<config>_<kernel>.json), or None when no such measurement exists."""
+def load_traffic(config, kernel, key="bytes_per_launch", prefix="profiles"):
+    """HBM bytes of `kernel` at `config` (per launch, or per fit with key="bytes_per_fit") from a
+    committed PMC summary (profiles/traffic/<config>_<kernel>.json, tools/traffic_summary.py), or
+    None when no such measurement exists."""
     path = os.path.join(ROOT, prefix, "traffic", f"{config}_{kernel}.json")
     if os.path.exists(path):
         with open(path) as f:
-            return json.load(f).get("bytes_per_launch")
+            return json.load(f).get(key)
     return None
 
 
@@ -312,7 +313,7 @@ def main():
                 "frac": co_achieved / I8_MFMA_PEAK_TOPS,
                 "ops_per_fit": co_ops / args.steps,
                 "ms_per_fit": co_ms_tot / args.steps,
-                "traffic": load_traffic(args.config, "cc_coassoc"),
+                "traffic": load_traffic(args.config, "cc_coassoc", key="bytes_per_fit"),
                 "note": "the 20-bin histogram (K5) is fused into this kernel's epilogue: no HBM pass",
             },
             "kernels_ms_per_step": {k: v[1] / args.steps for k, v in timers.items()},
