@@ -1119,7 +1119,11 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         KM_ACC(5, s5, s6);
       }
 #ifdef CC_KM_STAMPS
+#ifdef CC_KM_STAMPS_NARROW
+      if (ncols <= 32 && lane == 0 && a.stats)  // narrow sweeps only, every workgroup
+#else
       if (blockIdx.x == 0 && lane == 0 && a.stats)
+#endif
         for (int k = 0; k < 7; ++k) atomicAdd(&a.stats[8 + 8 * wave + k], st_acc[k]);
 #endif
       estep_flush(S, tid, es);
@@ -1343,6 +1347,12 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
 #ifdef CC_KM_STAMPS
       KM_STAMP(pp1);
       if (blockIdx.x == 0 && tid == 0 && a.stats) atomicAdd(&a.stats[73], pp1 - pp0);
+      // sweep cycles and counts by width (active 32-slot waves 1..8), all workgroups
+      if (tid == 0 && a.stats) {
+        const int wv = (ncols + 31) / 32;
+        atomicAdd(&a.stats[80 + wv], pp1 - swp);
+        atomicAdd(&a.stats[96 + wv], 1ull);
+      }
 #endif
     }
 

@@ -33,3 +33,8 @@ print("post-processing cycles (wg0):", st[73] / 1e6, "M")
 it = cc.kmeans_n_iter_.cpu().numpy()
 print("n_iter per K (mean/max over h):", {K: (round(float(it[k].mean()), 1), int(it[k].max()))
                                           for k, K in enumerate(cfg["Ks"])})
+cyc = st[80:89].astype(float)
+cnt = st[96:105].astype(float)
+tot = max(cyc.sum(), 1)
+print("sweeps by active waves (1..8): count / share of sweep cycles / mean Mcycles:",
+      {w: (int(cnt[w]), f"{100 * cyc[w] / tot:.0f}%", round(cyc[w] / max(cnt[w], 1) / 1e6, 2)) for w in range(1, 9)})
