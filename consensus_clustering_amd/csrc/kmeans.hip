@@ -74,6 +74,14 @@ constexpr int KMAX = 127;
 constexpr int DSD = CW + 4;         // distance-tile row stride (floats): 16-B rows, conflict-free b128
 constexpr int NRING = 4;            // X tile ring: t+1 (gather), t (dist), t-2 (M-step)
 constexpr int US = CC_KM_USTRIDE;
+// step-dealing cost units (a Lloyd step of K = 20 costs 72, a seeding step 20): the distance
+// MFMAs and the M-step of a wave's own slots, measured in the same units from the phase stamps
+#ifndef KM_COST_DIST
+#define KM_COST_DIST 105
+#endif
+#ifndef KM_COST_MSTEP
+#define KM_COST_MSTEP 65
+#endif
 
 // Diagnostic build only (-DCC_KM_STAMPS): per-wave cycle accounting of the sweep phases of
 // workgroup 0, added into stats[8 + 8 * wave + k] (k: issue, dist, estep, mstep, commit,
@@ -786,7 +794,19 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
   // deal the steps to the waves (LPT: heaviest first onto the least loaded wave)
   int wcost[NW];
   for (int w = 0; w < NW; ++w) {
+    // a wave that owns slots also runs their distance MFMAs (and their M-step when a running
+    // centre is among them): in narrow sweeps the E-steps then go to the idle waves
     wcost[w] = 0;
+#ifndef CC_KM_NO_OWNER_COST
+    if (32 * w < nc) {
+      wcost[w] = KM_COST_DIST;
+      for (int c = 32 * w; c < min(nc, 32 * w + 32); ++c)
+        if (S.scl[c] >= 0) {
+          wcost[w] += KM_COST_MSTEP;
+          break;
+        }
+    }
+#endif
     S.nlw[w] = S.nsw[w] = 0;
     for (int i = 0; i < NLS; ++i) S.lstep[w][i] = 0xFF;
     for (int i = 0; i < NSS; ++i) S.sstep[w][i][0] = S.sstep[w][i][1] = 0xFF;
