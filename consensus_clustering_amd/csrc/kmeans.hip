@@ -146,6 +146,7 @@ struct State {
   unsigned iw0[IMAX], iw1[IMAX];               // packed item words (see EState)
   unsigned char lstep[NW][NLS], sstep[NW][NSS][2];  // E-step steps of each wave (item; 0xFF none)
   unsigned char nlw[NW], nsw[NW];
+  signed char mtile[NW];  // slot tile whose M-step the wave runs (-1: none)
   short ioff[IMAX], incol[IMAX];
   double iinert[IMAX];
   unsigned ichanged[IMAX];
@@ -792,21 +793,26 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
   }
   S.rr = (first_skip >= 0) ? first_skip : (last >= 0 ? (last + 1) % P : S.rr);
   // deal the steps to the waves (LPT: heaviest first onto the least loaded wave)
+  // M-step owners: in a sweep with k <= NW/2 slot tiles, wave k + w runs the M-step of tile w
+  // (its own accumulators), so the distance owner's serial chain loses the M-step; otherwise
+  // every wave runs the M-step of its own tile
+  const int kt = (nc + 31) / 32;
+  const bool split_m = 2 * kt <= NW;
+  for (int w = 0; w < NW; ++w) S.mtile[w] = static_cast<signed char>(split_m ? -1 : (w < kt ? w : -1));
+  if (split_m)
+    for (int w = 0; w < kt; ++w) S.mtile[kt + w] = static_cast<signed char>(w);
   int wcost[NW];
   for (int w = 0; w < NW; ++w) {
-    // a wave that owns slots also runs their distance MFMAs (and their M-step when a running
-    // centre is among them): in narrow sweeps the E-steps then go to the idle waves
-    wcost[w] = 0;
-#ifndef CC_KM_NO_OWNER_COST
-    if (32 * w < nc) {
-      wcost[w] = KM_COST_DIST;
-      for (int c = 32 * w; c < min(nc, 32 * w + 32); ++c)
+    // the distance MFMAs of a wave's own slots and the M-step it runs count against it, so that
+    // in narrow sweeps the E-steps go to the idle waves, off those serial chains
+    wcost[w] = (32 * w < nc) ? KM_COST_DIST : 0;
+    const int mt = S.mtile[w];
+    if (mt >= 0)
+      for (int c = 32 * mt; c < min(nc, 32 * mt + 32); ++c)
         if (S.scl[c] >= 0) {
           wcost[w] += KM_COST_MSTEP;
           break;
         }
-    }
-#endif
     S.nlw[w] = S.nsw[w] = 0;
     for (int i = 0; i < NLS; ++i) S.lstep[w][i] = 0xFF;
     for (int i = 0; i < NSS; ++i) S.sstep[w][i][0] = S.sstep[w][i][1] = 0xFF;
@@ -985,10 +991,13 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
 #pragma unroll
       for (int dt = 0; dt < DP / 32; ++dt) sacc[dt] = v16f{};
       unsigned mcnt = 0;
+      // M-step slot tile of this wave (its own, or a distance owner's in narrow sweeps)
+      const int mt = __builtin_amdgcn_readfirstlane(static_cast<int>(S.mtile[wave]));
+      const int msl = 32 * mt + lr;
       int mycl = -1, myit = 0;
-      if (sl < ncols) {
-        myit = max(static_cast<int>(S.sitem[sl]), 0);
-        mycl = S.scl[sl];
+      if (mt >= 0 && msl < ncols) {
+        myit = max(static_cast<int>(S.sitem[msl]), 0);
+        mycl = S.scl[msl];
       }
       const bool mact = __ballot(mycl >= 0) != 0ull;  // wave-uniform: any running centre
       // pipeline prologue: tile 0 in the ring, indices of tile 1
@@ -1153,11 +1162,11 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         for (int dt = 0; dt < DP / 32; ++dt)
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
-            const int s2 = 32 * ct + (v & 3) + 8 * (v >> 2) + 4 * hh;
+            const int s2 = 32 * mt + (v & 3) + 8 * (v >> 2) + 4 * hh;
             Sm[s2 * DP + 32 * dt + lr] = sacc[dt][v] * a.inv_scale;
           }
         const unsigned tot = mcnt + __shfl_xor(mcnt, 32);
-        if (hh == 0) S.cnt[sl] = tot;
+        if (hh == 0) S.cnt[msl] = tot;
       }
       __syncthreads();
 
