@@ -36,3 +36,9 @@ for r in range(reps + 1):
         ts.append(a.elapsed_time(b))
 print(os.path.basename(os.environ.get("CCMI_LIB", "libccmi.so")), "kmeans ms", [round(t, 1) for t in ts],
       "sweeps", int(bk.stats[4]), flush=True)
+st = bk.stats.cpu().numpy()
+cyc, cnt = st[80:89].astype(float), st[96:105].astype(float)
+tot = max(cyc.sum(), 1)
+print("  sweeps by active waves: count / share of sweep cycles / mean Mcycles:",
+      {w: (int(cnt[w]), f"{100 * cyc[w] / tot:.0f}%", round(cyc[w] / max(cnt[w], 1) / 1e6, 2)) for w in range(1, 9)
+       if cnt[w]}, flush=True)
