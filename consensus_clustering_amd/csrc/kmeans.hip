@@ -82,6 +82,15 @@ constexpr int US = CC_KM_USTRIDE;
 #ifndef KM_COST_MSTEP
 #define KM_COST_MSTEP 65
 #endif
+#ifndef KM_COST_LBASE
+#define KM_COST_LBASE 24
+#endif
+#ifndef KM_COST_LCHUNK
+#define KM_COST_LCHUNK 16
+#endif
+#ifndef KM_COST_SSTEP
+#define KM_COST_SSTEP 20
+#endif
 
 // Diagnostic build only (-DCC_KM_STAMPS): per-wave cycle accounting of the sweep phases of
 // workgroup 0, added into stats[8 + 8 * wave + k] (k: issue, dist, estep, mstep, commit,
@@ -823,7 +832,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     for (int q = 0; q < NW; ++q)
       if (S.nlw[q] < NLS && (w < 0 || wcost[q] < wcost[w])) w = q;
     S.lstep[w][S.nlw[w]++] = static_cast<unsigned char>(it);
-    wcost[w] += (S.incol[it] + 7) / 8 * 16 + 24;
+    wcost[w] += (S.incol[it] + 7) / 8 * KM_COST_LCHUNK + KM_COST_LBASE;
   }
   int open_w = -1;
   for (int it = 0; it < ni; ++it) {
@@ -837,7 +846,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     for (int q = 0; q < NW; ++q)
       if (S.nsw[q] < NSS && (w < 0 || wcost[q] < wcost[w])) w = q;
     S.sstep[w][S.nsw[w]++][0] = static_cast<unsigned char>(it);
-    wcost[w] += 20;
+    wcost[w] += KM_COST_SSTEP;
     open_w = w;
   }
   S.nitems = ni;
