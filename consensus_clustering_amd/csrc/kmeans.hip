@@ -31,14 +31,19 @@
 // counts a one-hot x ones MFMA.  All decisions (argmin, potentials, convergence, relocation,
 // best-of-init) are f32/f64 as in sklearn.
 //
-// The 8 waves are uniform.  Wave w owns centroid slots 32w..32w+31 (register-resident f16
-// A fragments) and, per tile iteration t (one barrier each), does
-//   dist MFMA of tile t -> LDS distance tile (double buffer),
-//   E-step of tile t-1 (all 512 threads: thread = (row, work item); argmin per Lloyd
-//     problem, min-with-closest per seeding candidate),
-//   M-step of tile t-2 (one-hot A from the E-step labels, B = the X tile read back with
-//     ds_read_b64_tr_b16 from the same swizzled image the distance reads row-wise),
-//   and the gather of tile t+1 into a 4-slot ring.
+// The 8 waves have two roles, one wave of each per SIMD, each role in its own tile loop (one
+// barrier per tile in both, so their register sets never overlap and one role's vector chain
+// runs while the other's MFMAs occupy the matrix pipe).  Per tile iteration t:
+//   distance waves 0..3: the gather of tile t+1 into a 4-slot ring (LDS-DMA), the distance
+//     MFMAs of tile t for slot tiles w and w+4 (register-resident f16 A fragments, one B read
+//     per k-step for both) -> LDS distance tile (double buffer), and a share of the E-steps;
+//   E/M waves 4..7: most E-steps of tile t-1 (thread = (row, work item); argmin per Lloyd
+//     problem, min-with-closest per seeding candidate) and the M-steps of tile t-2 for slot
+//     tiles q and q+4 (one-hot A from the E-step labels, B = the X tile read back with
+//     ds_read_b64_tr_b16 from the same swizzled image the distance reads row-wise, one B read
+//     for both tiles).
+// The E-steps are dealt by LPT on a cost model in which the distance waves start with the cost
+// of their MFMAs (KM_COST_DIST per slot tile) and the E/M waves with their M-steps.
 // Nothing crosses workgroups, so results do not depend on scheduling, on how the units are
 // split over launches or over GPUs.
 #include <hip/hip_runtime.h>
@@ -63,10 +68,14 @@ typedef __attribute__((address_space(3))) s4 lds_s4;
 
 constexpr int NT = 512;
 constexpr int NW = 8;
+constexpr int NDW = 4;              // distance waves 0..3 (gather + distance MFMAs), one per SIMD
+constexpr int NEW = NW - NDW;       // E/M waves 4..7 (E-steps + M-step MFMAs), one per SIMD
 constexpr int RT = 32;              // rows per tile (one MFMA row block)
-constexpr int CW = 256;             // centroid slots per sweep (8 waves x 32)
-constexpr int NLS = 4;              // E-step Lloyd steps per wave (one Lloyd item each)
-constexpr int NSS = 4;              // E-step seeding steps per wave (two seeding items each)
+constexpr int CW = 256;             // centroid slots per sweep (8 slot tiles of 32)
+constexpr int NLS = 8;              // E-step Lloyd steps per E/M wave (one Lloyd item each)
+constexpr int NSS = 8;              // E-step seeding steps per E/M wave (two seeding items each)
+constexpr int NLS_D = 3;            // ... per distance wave (they take a share of the E-steps;
+constexpr int NSS_D = 2;            //     more spill their A fragments at d = 128)
 constexpr int IMAX = 64;            // work items per sweep
 constexpr int PMAX = CC_KM_PMAX;    // problems per unit
 constexpr int TMAX = 6;             // max local trials: 2 + floor(ln 127)
@@ -77,7 +86,7 @@ constexpr int US = CC_KM_USTRIDE;
 // step-dealing cost units (a Lloyd step of K = 20 costs 72, a seeding step 20): the distance
 // MFMAs and the M-step of a wave's own slots, measured in the same units from the phase stamps
 #ifndef KM_COST_DIST
-#define KM_COST_DIST 105
+#define KM_COST_DIST 80
 #endif
 #ifndef KM_COST_MSTEP
 #define KM_COST_MSTEP 65
@@ -155,7 +164,7 @@ struct State {
   unsigned iw0[IMAX], iw1[IMAX];               // packed item words (see EState)
   unsigned char lstep[NW][NLS], sstep[NW][NSS][2];  // E-step steps of each wave (item; 0xFF none)
   unsigned char nlw[NW], nsw[NW];
-  signed char mtile[NW];  // slot tile whose M-step the wave runs (-1: none)
+  int4 sdesc[NW][NSS][2];  // seeding step descriptors of the sweep (see estep)
   short ioff[IMAX], incol[IMAX];
   double iinert[IMAX];
   unsigned ichanged[IMAX];
@@ -186,6 +195,7 @@ struct Lay {
   static constexpr int OFF_ST = OFF_XN + NRING * 64 * 4;
   static constexpr int TOTAL = OFF_ST + ((sizeof(State) + 15) / 16) * 16;
   static_assert(TOTAL <= 163840, "LDS budget");
+  static_assert(NSS % 4 == 0 && (NSS_D < 4 || NSS_D % 4 == 0), "seeding steps are read in batches");
 };
 
 // Byte offset of 16-B chunk `ch` of tile row `row` in one f16 image (DP/8 chunks per row).
@@ -253,7 +263,7 @@ template <int DP>
 struct Gather {
   static constexpr int IMG = RT * DP * 2;
   static constexpr int NI = (2 * IMG) / 1024;          // pieces per tile (hi + lo)
-  static constexpr int PER = (NI + NW - 1) / NW;       // pieces per wave
+  static constexpr int PER = (NI + NDW - 1) / NDW;     // pieces per distance wave
   static constexpr int ROWB = 2 * DP;                  // bytes per image row
 };
 
@@ -269,7 +279,7 @@ __device__ __forceinline__ void idx_issue(const KArgs& a, const int32_t* idx, in
   using GA = Gather<DP>;
 #pragma unroll
   for (int j = 0; j < GA::PER; ++j) {
-    const int k = wave + NW * j;
+    const int k = wave + NDW * j;
     const int B = 1024 * k + 16 * lane;
     const int off = B % GA::IMG;
     I.src[j] = idx[min(r0 + off / GA::ROWB, a.m - 1)];
@@ -294,45 +304,58 @@ __device__ __forceinline__ void dma_piece(const void* g, const void* lds_dst, in
     asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g));
 }
 
+// DMA source addresses of one tile (computed before anything else is issued, so that the
+// compiler's wait for the index registers, loaded one iteration earlier, precedes every piece).
 template <int DP>
-__device__ __forceinline__ void tile_dma(const KArgs& a, const TileIdx<DP>& I, char* slot, float* xn,
-                                         int wave, int lane) {
+struct TileAddr {
+  const uint16_t* src[Gather<DP>::PER];
+  const float* xsrc;
+};
+
+template <int DP>
+__device__ __forceinline__ void tile_addr(const KArgs& a, const TileIdx<DP>& I, int wave, int lane,
+                                          TileAddr<DP>& A) {
   using GA = Gather<DP>;
-  // Every address first: the compiler's wait for the index registers (loaded last iteration)
-  // must come before the first DMA, or it would also wait for the DMA (untracked, in order).
-  const uint16_t* src[GA::PER];
   int ln = lane;
   asm volatile("" : "+v"(ln));  // recompute the per-lane chunk offsets (cheap) rather than hold them
 #pragma unroll
   for (int j = 0; j < GA::PER; ++j) {
-    const int k = wave + NW * j;
+    const int k = wave + NDW * j;
     const int B = 1024 * k + 16 * ln;
     const int part = B / GA::IMG, off = B - part * GA::IMG;
     const int row = off / GA::ROWB, ch = ((off % GA::ROWB) >> 4) ^ xsw<DP>(row);
-    src[j] = a.Xhl + static_cast<size_t>(I.src[j]) * (2 * DP) + part * DP + 8 * ch;
+    A.src[j] = a.Xhl + static_cast<size_t>(I.src[j]) * (2 * DP) + part * DP + 8 * ch;
   }
-  const float* xsrc = a.xnorm + I.xsrc;
+  A.xsrc = a.xnorm + I.xsrc;
+}
+
+// Keeps the pieces' address registers allocated up to this point (after the end-of-iteration
+// wait): the compiler treats an inline-asm operand as possibly still being read, and would
+// put a vmcnt(0) in front of any instruction that reuses one of those registers earlier.
+template <int DP>
+__device__ __forceinline__ void tile_addr_hold(const TileAddr<DP>& A) {
+#pragma unroll
+  for (int j = 0; j < Gather<DP>::PER; ++j) asm volatile("" ::"v"(A.src[j]));
+  asm volatile("" ::"v"(A.xsrc));
+}
+
+// The tile's pieces, issued last in the gather block: no VALU after them overwrites an address
+// register before the end-of-iteration wait (the compiler would wait vmcnt(0) for that).
+template <int DP>
+__device__ __forceinline__ void tile_issue(const TileAddr<DP>& A, char* slot, float* xn, int wave) {
+  using GA = Gather<DP>;
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int j = 0; j < GA::PER; ++j)
-    if (wave + NW * j < GA::NI) dma_piece(src[j], slot + 1024 * (wave + NW * j), 16);  // wave-uniform
-  if (wave == NW - 1) dma_piece(xsrc, xn, 4);
+    if (wave + NDW * j < GA::NI) dma_piece(A.src[j], slot + 1024 * (wave + NDW * j), 16);  // wave-uniform
+  if (wave == NDW - 1) dma_piece(A.xsrc, xn, 4);
+  __builtin_amdgcn_sched_barrier(0);
 }
 
-__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Wait for this iteration's DMA pieces and loads but not for the label/potential stores the
-// E-step issued after them (vmcnt drains in order; `younger` = store instructions issued
-// after the last load, wave-uniform): store acks would otherwise be exposed every tile.
-__device__ __forceinline__ void dma_wait_leaving(int younger) {
-  if (younger >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (younger >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (younger >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (younger >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if (younger >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if (younger >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
+// vmcnt(0) through the builtin (not inline asm): the compiler's waitcnt model then knows that
+// nothing is outstanding, so it puts no wait of its own after the next tile's DMA pieces (which
+// it cannot see) for loads that have already landed.
+__device__ __forceinline__ void dma_wait() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 // A fragments of one centroid slot: lane (r, h) holds dims 16s + 8h + j of its slot's centre.
 template <int DP>
@@ -530,8 +553,9 @@ __device__ void kpp_select(const KArgs& a, St& S, int p, const float* closest, i
 // then flushed (f64 half-wave sum) into the item's f64 accumulator in LDS (S.iinert).  f32
 // partials keep 8 VGPRs instead of 16: with f64 partials the kernel spilled, and every spill
 // reload drained the LDS-DMA pipeline (vmcnt(0)).
+template <int NL, int NS>
 struct EState {
-  float iaccL[NLS], iaccS[NSS];
+  float iaccL[NL], iaccS[NS];
 };
 constexpr int FLUSH = 32;  // tiles per f32 partial
 
@@ -541,64 +565,68 @@ __device__ __forceinline__ int iw_prob(unsigned w) { return (w >> 16) & 0x3F; }
 __device__ __forceinline__ int iw_kind(unsigned w) { return (w >> 24) & 3; }
 __device__ __forceinline__ int iw_buf(unsigned w) { return (w >> 30) & 1; }
 
+// Seeding step descriptor (one per wave, step and half-wave, every entry initialised; built
+// once per sweep so that a step costs one LDS read instead of three dependent ones, and all
+// steps' reads are issued together, unconditionally): x = closest-distance column read (float
+// offset in dbuf), z = column written, y = w = distance column (CW, the +inf chunk, when the
+// half-wave has no item) | flags << 16, flags = 1 (item) | 2 (kind IK_SEED: min with the
+// closest distance).  The prefetch reads (x, y), the E-step (z, w).
+__device__ __forceinline__ int4 seed_desc(const KArgs& a, const State& S, int it, int T1) {
+  if (it == 0xFF) return make_int4(0, CW, 0, CW);
+  const unsigned w0 = S.iw0[it], w1 = S.iw1[it];
+  const int slot = w1 & 31;
+  const int dcf = iw_off(w0) | ((1 | ((iw_kind(w0) == IK_SEED) ? 2 : 0)) << 16);
+  return make_int4((slot * T1 + ((w1 >> 8) & 7)) * a.lsm, dcf, (slot * T1 + ((w1 >> 11) & 7)) * a.lsm, dcf);
+}
+
 // Closest distances of the seeding items of tile tp (issued one iteration before its E-step).
-template <int DP>
-__device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, int tp, int T, int tidl,
-                                               const float* dbuf, int T1, unsigned (&pre)[NSS]) {
-  const int m = a.m;
+template <int NS>
+__device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, int tp, int T, int tidl, int ns,
+                                               const float* dbuf, unsigned (&pre)[NS]) {
   const int erow = tp * RT + (tidl & (RT - 1));
-  const bool eok = (tp >= 0 && tp < T) && erow < m;
+  const bool eok = (tp >= 0 && tp < T) && erow < a.m;
   const int w = (tidl >> 6) & 7, hh = (tidl >> 5) & 1;  // tidl is opaque: steps re-read from LDS
-  const int ns = __builtin_amdgcn_readfirstlane(S.nsw[w]);
-  if constexpr (DP == 128) {
-    // Branch-free over the steps: the step words of all steps are read together (one LDS
-    // round trip per level instead of one per step and level).  Measured per row width: C3
-    // (d = 128) 2557 -> 2525 ms; at d = 32 / 64 (C5, C2) the same code was 9 % / 4 % slower,
-    // so the narrow instantiations keep the per-step chain.
 #pragma unroll
-    for (int i = 0; i < NSS; ++i) pre[i] = 0;
-    if (ns == 0) return;  // wave-uniform: Lloyd-only sweeps
-    int its[NSS];
-    unsigned w0s[NSS], w1s[NSS];
+  for (int i = 0; i < NS; ++i) pre[i] = 0;
 #pragma unroll
-    for (int i = 0; i < NSS; ++i) its[i] = S.sstep[w][i][hh];
+  for (int i0 = 0; i0 < NS; i0 += (NS < 4 ? NS : 4)) {  // wave-uniform: only the batches in use
+    if (i0 >= ns) break;
+    constexpr int B = NS < 4 ? NS : 4;
+    int2 d[B];
 #pragma unroll
-    for (int i = 0; i < NSS; ++i) {
-      w0s[i] = S.iw0[its[i] & (IMAX - 1)];
-      w1s[i] = S.iw1[its[i] & (IMAX - 1)];
-    }
+    for (int i = 0; i < B; ++i) d[i] = *reinterpret_cast<const int2*>(&S.sdesc[w][i0 + i][hh].x);  // in flight together
 #pragma unroll
-    for (int i = 0; i < NSS; ++i) {
-      if (i < ns && eok && its[i] != 0xFF && iw_kind(w0s[i]) == IK_SEED)
-        pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(w1s[i] & 31) * T1 + ((w1s[i] >> 8) & 7)) * a.lsm + erow]);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NSS; ++i) {
-      pre[i] = 0;
-      if (i >= ns) break;
-      const int it = S.sstep[w][i][hh];
-      if (eok && it != 0xFF && iw_kind(S.iw0[it]) == IK_SEED) {
-        const unsigned w1 = S.iw1[it];
-        pre[i] = __float_as_uint(dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 8) & 7)) * a.lsm + erow]);
-      }
-    }
+    for (int i = 0; i < B; ++i)
+      if (eok && (d[i].y & (2 << 16))) pre[i0 + i] = __float_as_uint(dbuf[static_cast<unsigned>(d[i].x) + erow]);
   }
 }
 
-// strict-< argmin update of (best, lab) with the 4 values of an aligned chunk at slot c
-__device__ __forceinline__ void amin4(const float4& v, int c, float& best, int& lab) {
-  if (v.x < best) { best = v.x; lab = c; }
-  if (v.y < best) { best = v.y; lab = c + 1; }
-  if (v.z < best) { best = v.z; lab = c + 2; }
-  if (v.w < best) { best = v.w; lab = c + 3; }
+// strict-< argmin of 4 aligned chunks (16 slots, columns col[u] .. col[u] + 3, increasing in u)
+// as a tree (dependency depth 4 instead of 16): ties keep the lower slot at every level.
+__device__ __forceinline__ void amin16(const float4 (&v)[4], const int (&col)[4], float& best, int& lab) {
+  float bv[4];
+  int bi[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float m0 = v[u].x, m1 = v[u].z;
+    int i0 = col[u], i1 = col[u] + 2;
+    if (v[u].y < m0) { m0 = v[u].y; i0 = col[u] + 1; }
+    if (v[u].w < m1) { m1 = v[u].w; i1 = col[u] + 3; }
+    if (m1 < m0) { m0 = m1; i0 = i1; }
+    bv[u] = m0;
+    bi[u] = i0;
+  }
+  if (bv[1] < bv[0]) { bv[0] = bv[1]; bi[0] = bi[1]; }
+  if (bv[3] < bv[2]) { bv[2] = bv[3]; bi[2] = bi[3]; }
+  if (bv[2] < bv[0]) { bv[0] = bv[2]; bi[0] = bi[2]; }
+  if (bv[0] < best) { best = bv[0]; lab = bi[0]; }
 }
 
-template <int DP>
+template <int DP, int NL, int NS>
 __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int T, int tidl, const float* Dt,
-                                      uint8_t* Ls, const float* XN, uint8_t* glab, float* dbuf, int T1,
-                                      const unsigned (&pre)[NSS], const unsigned (&lw)[NLS], int nl,
-                                      EState& es) {
+                                      uint8_t* Ls, const float* XN, uint8_t* glab, float* dbuf,
+                                      const unsigned (&pre)[NS], const unsigned (&lw)[NL], int nl, int ns,
+                                      EState<NL, NS>& es) {
   if (t < 1 || t > T) return;
   const int m = a.m;
   const int te = t - 1;
@@ -610,17 +638,39 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
   uint8_t* lsb = Ls + (te & 1) * (IMAX * RT);
   const float xnr = XN[(te % NRING) * 64 + ler];
   constexpr float INF = __builtin_huge_valf();
+  // seeding steps first (one item per half-wave): descriptors and distances of every step in
+  // flight together, then min with the closest distance, store for the potential and the next
+  // k-means++ draw
+#pragma unroll
+  for (int i0 = 0; i0 < NS; i0 += (NS < 4 ? NS : 4)) {  // wave-uniform: only the batches in use
+    if (i0 >= ns) break;
+    constexpr int B = NS < 4 ? NS : 4;
+    int2 d[B];
+    float dd[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) d[i] = *reinterpret_cast<const int2*>(&S.sdesc[w][i0 + i][hh].z);
+#pragma unroll
+    for (int i = 0; i < B; ++i) dd[i] = drow[d[i].y & 0xFFFF];
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const float dist = fmaxf(xnr + dd[i], 0.f);
+      const float dm = (d[i].y & (2 << 16)) ? fminf(__uint_as_float(pre[i0 + i]), dist) : dist;
+      if (eok && (d[i].y & (1 << 16))) {
+        dbuf[static_cast<unsigned>(d[i].x) + erow] = dm;
+        es.iaccS[i0 + i] += dm;
+      }
+    }
+  }
   // Lloyd steps (wave-uniform words, hoisted for the sweep)
 #pragma unroll
-  for (int i = 0; i < NLS; ++i) {
+  for (int i = 0; i < NL; ++i) {
     if (i >= nl) break;
     const unsigned ww = lw[i];
-    const int it = S.lstep[w][i];
     const int off = iw_off(ww), C = (iw_K(ww) + 3) >> 2, h0 = (C + 1) >> 1;
     const int base = off + (hh ? 4 * h0 : 0), cnt = hh ? C - h0 : h0;
     float best = INF;
     int lab = 0;
-    for (int j0 = 0; j0 < h0; j0 += 4) {  // 4 chunk reads in flight, then the compare chain
+    for (int j0 = 0; j0 < h0; j0 += 4) {  // 4 chunk reads in flight, then a tree argmin
       int col[4];
       float4 v[4];
 #pragma unroll
@@ -628,8 +678,7 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
         col[u] = (j0 + u < cnt) ? base + 4 * (j0 + u) : CW;  // CW..CW+3 hold +inf
         v[u] = *reinterpret_cast<const float4*>(drow + col[u]);
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) amin4(v[u], col[u], best, lab);
+      amin16(v, col, best, lab);
     }
     // merge the halves (v_permlane32_swap: lane i <-> i^32 without LDS): lower value, ties to
     // the lower slot (half 0 holds the lower slots)
@@ -647,73 +696,176 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
         glab[(static_cast<size_t>(2 * iw_prob(ww) + iw_buf(ww))) * a.lsm + erow] = static_cast<uint8_t>(lab);
         es.iaccL[i] += xnr + best;
       }
-      lsb[it * RT + ler] = eok ? static_cast<uint8_t>(lab) : 0xFF;
-    }
-  }
-  // seeding steps (one item per half-wave)
-  const int ns = __builtin_amdgcn_readfirstlane(S.nsw[w]);
-  if constexpr (DP == 128) {  // see estep_prefetch: branch-free step words at d = 128 only
-    if (ns == 0) return;  // wave-uniform: Lloyd-only sweeps
-    // step words and distances of all steps first (branch-free: one LDS round trip per level)
-    int its[NSS];
-    unsigned w0s[NSS], w1s[NSS];
-    float dd[NSS];
-#pragma unroll
-    for (int i = 0; i < NSS; ++i) its[i] = S.sstep[w][i][hh];
-#pragma unroll
-    for (int i = 0; i < NSS; ++i) {
-      const bool has = i < ns && its[i] != 0xFF;
-      w0s[i] = has ? S.iw0[its[i] & (IMAX - 1)] : 0u;
-      w1s[i] = has ? S.iw1[its[i] & (IMAX - 1)] : 0u;
-    }
-#pragma unroll
-    for (int i = 0; i < NSS; ++i) dd[i] = drow[iw_off(w0s[i])];
-#pragma unroll
-    for (int i = 0; i < NSS; ++i) {
-      if (i >= ns) break;
-      const bool has = its[i] != 0xFF;
-      const unsigned ww = w0s[i], w1 = w1s[i];
-      const float dist = fmaxf(xnr + dd[i], 0.f);
-      const float dm = (iw_kind(ww) == IK_SEED) ? fminf(__uint_as_float(pre[i]), dist) : dist;
-      if (eok && has) {
-        dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 11) & 7)) * a.lsm + erow] = dm;
-        es.iaccS[i] += dm;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NSS; ++i) {
-      if (i >= ns) break;
-      const int it = S.sstep[w][i][hh];
-      const bool has = it != 0xFF;
-      const unsigned ww = has ? S.iw0[it] : 0u, w1 = has ? S.iw1[it] : 0u;
-      const float dist = fmaxf(xnr + drow[iw_off(ww)], 0.f);
-      const float dm = (iw_kind(ww) == IK_SEED) ? fminf(__uint_as_float(pre[i]), dist) : dist;
-      if (eok && has) {
-        dbuf[(static_cast<size_t>(w1 & 31) * T1 + ((w1 >> 11) & 7)) * a.lsm + erow] = dm;
-        es.iaccS[i] += dm;
-      }
+      lsb[iw_prob(ww) * RT + ler] = eok ? static_cast<uint8_t>(lab) : 0xFF;  // M-step labels, by problem
     }
   }
 }
 
 // Add the f32 partials into the items' f64 accumulators (each item has exactly one
 // contributing half-wave, so lane 0 of it is the only writer) and restart them.
-__device__ __forceinline__ void estep_flush(State& S, int tid, EState& es) {
+template <int NL, int NS>
+__device__ __forceinline__ void estep_flush(State& S, int tid, EState<NL, NS>& es) {
   const int er = tid & (RT - 1), hh = (tid >> 5) & 1, w = tid >> 6;
   const int nl = S.nlw[w], ns = S.nsw[w];
 #pragma unroll
-  for (int i = 0; i < NLS; ++i) {
+  for (int i = 0; i < NL; ++i) {
     const double v = half_sum(static_cast<double>(es.iaccL[i]));
     if (i < nl && er == 0 && hh == 0) S.iinert[S.lstep[w][i]] += v;
     es.iaccL[i] = 0.f;
   }
 #pragma unroll
-  for (int i = 0; i < NSS; ++i) {
+  for (int i = 0; i < NS; ++i) {
     const double v = half_sum(static_cast<double>(es.iaccS[i]));
     if (i < ns && er == 0 && S.sstep[w][i][hh] != 0xFF) S.iinert[S.sstep[w][i][hh]] += v;
     es.iaccS[i] = 0.f;
   }
+}
+
+// A fragments of slot sl (register-resident for the sweep): a candidate row (exact f32 row of
+// X), a running centre, or a dummy / alignment / unused slot (zero centre, +inf norm).
+template <int DP>
+__device__ __forceinline__ void slot_frags(const KArgs& a, const State& S, const float* cen, int sl, int ncols,
+                                           int hh, h8 (&ah)[DP / 16], h8 (&al)[DP / 16]) {
+  int sr = INT_MIN;
+  if (sl < ncols) sr = S.srow[sl];
+  const bool ok = sr != INT_MIN;
+  const float* src = (sr >= 0) ? a.X + static_cast<size_t>(sr) * DP
+                               : cen + static_cast<size_t>(ok ? -sr - 1 : 0) * DP;
+  afrag_load<DP>(ah, al, src, ok, hh, a.scale);
+}
+
+// Distance wave: x.c of the tile's 32 rows against NS slot tiles (w, w + NDW) on f16 MFMA
+// (xh.ch + xh.cl + xl.ch), one B operand read per k-step shared by the NS tiles, then
+// D = |c|^2 - 2 x.c into the LDS distance tile (row lr, 4 slots per b128 store).
+template <int DP, int NS>
+__device__ __forceinline__ void dist_tiles(const KArgs& a, const State& S, const char* xs, float* dtile, int w,
+                                           int lane, const h8 (&ah0)[DP / 16], const h8 (&al0)[DP / 16],
+                                           const h8 (&ah1)[DP / 16], const h8 (&al1)[DP / 16]) {
+  using LY = Lay<DP>;
+  __builtin_amdgcn_s_setprio(1);  // MFMA-dense block first in the SIMD arbiter
+  v16f acc0 = {}, acc1 = {};
+  int lno = lane;
+  asm volatile("" : "+v"(lno));  // per-lane offsets recomputed here (cheap), never held or spilled
+  const int lro = lno & 31, hh = lno >> 5;
+  // B operands one k-step ahead of the MFMAs (bounded: 16 VGPRs in flight)
+  h8 bh = *reinterpret_cast<const h8*>(xs + xoff<DP>(lro, hh));
+  h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + xoff<DP>(lro, hh));
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    h8 nh = bh, nl = bl;
+    if (s + 1 < DP / 16) {
+      const int off = xoff<DP>(lro, 2 * (s + 1) + hh);
+      nh = *reinterpret_cast<const h8*>(xs + off);
+      nl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
+    }
+    acc0 = mfma16(ah0[s], bl, acc0);
+    if constexpr (NS == 2) acc1 = mfma16(ah1[s], bl, acc1);
+    acc0 = mfma16(al0[s], bh, acc0);
+    if constexpr (NS == 2) acc1 = mfma16(al1[s], bh, acc1);
+    acc0 = mfma16(ah0[s], bh, acc0);
+    if constexpr (NS == 2) acc1 = mfma16(ah1[s], bh, acc1);
+    __builtin_amdgcn_sched_barrier(0);
+    bh = nh;
+    bl = nl;
+  }
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    const v16f& acc = j ? acc1 : acc0;
+    const int ct = w + NDW * j;
+    float* drow = dtile + lro * DSD + 32 * ct + 4 * hh;
+    const float* cn = S.cnorm + 32 * ct + 4 * hh;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // slots 8g + 4hh .. +3 of the tile: one b128 store
+      const float4 c4 = *reinterpret_cast<const float4*>(cn + 8 * g);
+      float4 d;
+      d.x = c4.x - a.dscale * acc[4 * g];
+      d.y = c4.y - a.dscale * acc[4 * g + 1];
+      d.z = c4.z - a.dscale * acc[4 * g + 2];
+      d.w = c4.w - a.dscale * acc[4 * g + 3];
+      *reinterpret_cast<float4*>(drow + 8 * g) = d;
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// E/M wave: one-hot A operand of the lane's slot (cluster mycl) for 8 rows of its 16-row k-block
+// s2 of a tile (f16 1.0 where label == mycl), and their count.
+__device__ __forceinline__ h8 onehot8(const uint8_t* lsb, int s2, int hh, int mycl, unsigned& mcnt) {
+  const unsigned long long lab8 = *reinterpret_cast<const unsigned long long*>(lsb + 16 * s2 + 8 * hh);
+  u32x4 ohu;
+  unsigned nb = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
+    const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
+    ohu[j] = ((b0 == mycl) ? 0x3C00u : 0u) | ((b1 == mycl) ? 0x3C000000u : 0u);
+    nb += (b0 == mycl) + (b1 == mycl);
+  }
+  mcnt += nb;
+  return __builtin_bit_cast(h8, ohu);
+}
+
+// E/M wave: M-step of NS slot tiles over one X tile: sums += one-hot(labels == cluster of the
+// lane's slot) x (xh + xl) on f16 MFMA, counts by popcount.  B is the X tile read back
+// transposed with ds_read_b64_tr_b16 from the swizzled image, once for the NS tiles.
+// lsb0 / lsb1: the labels of the problem each tile's lane slot belongs to.
+template <int DP, int NS>
+__device__ __forceinline__ void mstep_tiles(const char* xs, const uint8_t* lsb0, const uint8_t* lsb1, int lane,
+                                            int mycl0, int mycl1, v16f (&sacc0)[DP / 32], v16f (&sacc1)[DP / 32],
+                                            unsigned& mcnt0, unsigned& mcnt1) {
+  using LY = Lay<DP>;
+  int lanel = lane;
+  asm volatile("" : "+v"(lanel));
+  const int G = lanel >> 4, q = (lanel >> 2) & 3, pp = lanel & 3, hh = lanel >> 5;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    __builtin_amdgcn_sched_barrier(0);  // bounded working set: one k-half at a time
+    const h8 oh0 = onehot8(lsb0, s2, hh, mycl0, mcnt0);
+    h8 oh1 = oh0;
+    if constexpr (NS == 2) oh1 = onehot8(lsb1, s2, hh, mycl1, mcnt1);
+    const int row0 = 16 * s2 + 8 * (G >> 1) + q;
+    // transposed B reads one feature block ahead of its MFMAs
+    auto rd = [&](int dt, s4 (&r)[4]) __attribute__((always_inline)) {
+      const int chn = 4 * dt + 2 * (G & 1) + (pp >> 1);
+      const int a0 = xoff<DP>(row0, chn) + 8 * (pp & 1);
+      const int a1 = xoff<DP>(row0 + 4, chn) + 8 * (pp & 1);
+      r[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a0));
+      r[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a1));
+      r[2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a0));
+      r[3] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a1));
+    };
+    s4 rc[4], rn[4];
+    rd(0, rc);
+#pragma unroll
+    for (int dt = 0; dt < DP / 32; ++dt) {
+      if (dt + 1 < DP / 32) rd(dt + 1, rn);
+      const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(rc[0], rc[1], 0, 1, 2, 3, 4, 5, 6, 7));
+      const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(rc[2], rc[3], 0, 1, 2, 3, 4, 5, 6, 7));
+      sacc0[dt] = mfma16(oh0, bl, sacc0[dt]);
+      if constexpr (NS == 2) sacc1[dt] = mfma16(oh1, bl, sacc1[dt]);
+      sacc0[dt] = mfma16(oh0, bh, sacc0[dt]);
+      if constexpr (NS == 2) sacc1[dt] = mfma16(oh1, bh, sacc1[dt]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) rc[k] = rn[k];
+    }
+  }
+}
+
+// E/M wave, after the sweep: the un-averaged sums of slot tile ct into Sm, the counts of its
+// slots into S.cnt.
+template <int DP>
+__device__ __forceinline__ void msum_out(const KArgs& a, State& S, float* Sm, const v16f (&sacc)[DP / 32],
+                                         unsigned mcnt, int ct, int msl, int lr, int hh) {
+#pragma unroll
+  for (int dt = 0; dt < DP / 32; ++dt)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int s2 = 32 * ct + (v & 3) + 8 * (v >> 2) + 4 * hh;
+      Sm[s2 * DP + 32 * dt + lr] = sacc[dt][v] * a.inv_scale;
+    }
+  const unsigned tot = mcnt + __shfl_xor(mcnt, 32);
+  if (hh == 0) S.cnt[msl] = tot;
 }
 
 // Thread 0: admit waiting problems into free seeding slots, then pack the next sweep:
@@ -736,7 +888,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     if (S.st[p] != ST_SEED) continue;
     const int c = S.c[p];
     const int nt = (c == 0) ? 1 : S.ntr[p];
-    if (nc + nt > CW || ni + nt > IMAX || nss2 + nt > 2 * NW * NSS) continue;
+    if (nc + nt > CW || ni + nt > IMAX || nss2 + nt > 2 * (NEW * NSS + NDW * NSS_D)) continue;
     nss2 += nt;
     S.pitem[p] = static_cast<short>(ni);
     for (int t = 0; t < nt; ++t) {
@@ -769,7 +921,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     if (st != ST_RUN && st != ST_FINAL) continue;
     const int K = S.K[p], K4 = (K + 3) & ~3;
     const int off = (nc + 3) & ~3;
-    if (off + K4 > CW || ni + 1 > IMAX || nls + 1 > NW * NLS) {
+    if (off + K4 > CW || ni + 1 > IMAX || nls + 1 > NEW * NLS + NDW * NLS_D) {
       if (first_skip < 0) first_skip = p;
       continue;
     }
@@ -801,27 +953,21 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     if (st == ST_RUN) nm += a.m;
   }
   S.rr = (first_skip >= 0) ? first_skip : (last >= 0 ? (last + 1) % P : S.rr);
-  // deal the steps to the waves (LPT: heaviest first onto the least loaded wave)
-  // M-step owners: in a sweep with k <= NW/2 slot tiles, wave k + w runs the M-step of tile w
-  // (its own accumulators), so the distance owner's serial chain loses the M-step; otherwise
-  // every wave runs the M-step of its own tile
-  const int kt = (nc + 31) / 32;
-  const bool split_m = 2 * kt <= NW;
-  for (int w = 0; w < NW; ++w) S.mtile[w] = static_cast<signed char>(split_m ? -1 : (w < kt ? w : -1));
-  if (split_m)
-    for (int w = 0; w < kt; ++w) S.mtile[kt + w] = static_cast<signed char>(w);
+  // deal the E-steps to the waves (LPT: heaviest first onto the least loaded wave).  Distance
+  // wave w starts with the cost of its slot tiles' MFMAs (and takes at most NLS_D / NSS_D
+  // steps), E/M wave NDW + q with the M-steps of slot tiles q and q + NDW
   int wcost[NW];
   for (int w = 0; w < NW; ++w) {
-    // the distance MFMAs of a wave's own slots and the M-step it runs count against it, so that
-    // in narrow sweeps the E-steps go to the idle waves, off those serial chains
-    wcost[w] = (32 * w < nc) ? KM_COST_DIST : 0;
-    const int mt = S.mtile[w];
-    if (mt >= 0)
-      for (int c = 32 * mt; c < min(nc, 32 * mt + 32); ++c)
-        if (S.scl[c] >= 0) {
-          wcost[w] += KM_COST_MSTEP;
-          break;
-        }
+    wcost[w] = 0;
+    if (w < NDW)
+      for (int j = w; j < CW / 32; j += NDW) wcost[w] += (32 * j < nc) ? KM_COST_DIST : 0;
+    else
+      for (int j = w - NDW; j < CW / 32; j += NEW)
+        for (int c = 32 * j; c < min(nc, 32 * j + 32); ++c)
+          if (S.scl[c] >= 0) {
+            wcost[w] += KM_COST_MSTEP;
+            break;
+          }
     S.nlw[w] = S.nsw[w] = 0;
     for (int i = 0; i < NLS; ++i) S.lstep[w][i] = 0xFF;
     for (int i = 0; i < NSS; ++i) S.sstep[w][i][0] = S.sstep[w][i][1] = 0xFF;
@@ -830,7 +976,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     if (S.ikind[it] < IK_RUN) continue;
     int w = -1;
     for (int q = 0; q < NW; ++q)
-      if (S.nlw[q] < NLS && (w < 0 || wcost[q] < wcost[w])) w = q;
+      if (S.nlw[q] < (q < NDW ? NLS_D : NLS) && (w < 0 || wcost[q] < wcost[w])) w = q;
     S.lstep[w][S.nlw[w]++] = static_cast<unsigned char>(it);
     wcost[w] += (S.incol[it] + 7) / 8 * KM_COST_LCHUNK + KM_COST_LBASE;
   }
@@ -844,7 +990,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
     }
     int w = -1;
     for (int q = 0; q < NW; ++q)
-      if (S.nsw[q] < NSS && (w < 0 || wcost[q] < wcost[w])) w = q;
+      if (S.nsw[q] < (q < NDW ? NSS_D : NSS) && (w < 0 || wcost[q] < wcost[w])) w = q;
     S.sstep[w][S.nsw[w]++][0] = static_cast<unsigned char>(it);
     wcost[w] += KM_COST_SSTEP;
     open_w = w;
@@ -969,192 +1115,173 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         S.cnorm[tid] = (sr >= 0) ? a.xnorm[sr] : (sr == INT_MIN ? __builtin_huge_valf() : cenn[-sr - 1]);
       }
       if (tid < 2 * RT * 4) Dt[(tid >> 2) * DSD + CW + (tid & 3)] = __builtin_huge_valf();  // +inf chunk
-      // Every wave owns the slot tile ct = wave (32 slots): its centres as register-resident
-      // f16 A fragments (distances) and its M-step sums as MFMA accumulators.
-      const int ct = wave;
-      const int hh = lane >> 5, lr = lane & 31;
-      const int sl = 32 * ct + lr;
-      EState es;
-#pragma unroll
-      for (int i = 0; i < NLS; ++i) es.iaccL[i] = 0.f;
-      // this wave's Lloyd step words, wave-uniform for the whole sweep
-      const int nl = __builtin_amdgcn_readfirstlane(S.nlw[wave]);
-      unsigned lw[NLS];
-#pragma unroll
-      for (int i = 0; i < NLS; ++i)
-        lw[i] = __builtin_amdgcn_readfirstlane(i < nl ? S.iw0[S.lstep[wave][i]] : 0u);
-#pragma unroll
-      for (int i = 0; i < NSS; ++i) es.iaccS[i] = 0.f;
       if (tid < IMAX) S.iinert[tid] = 0.0;  // visible to the flushes after the prologue barrier
-      h8 ah[DP / 16], al[DP / 16];
-      const bool tact = 32 * ct < ncols;  // wave-uniform
-      {
-        int sr = INT_MIN;
-        if (sl < ncols) sr = S.srow[sl];
-        const bool ok = sr != INT_MIN;  // dummy / alignment slots: zero centre, +inf norm
-        const float* src = (sr >= 0) ? a.X + static_cast<size_t>(sr) * DP
-                                     : cen + static_cast<size_t>(ok ? -sr - 1 : 0) * DP;
-        afrag_load<DP>(ah, al, src, ok, hh, a.scale);
+      if (tid < NW * NSS * 2) {  // seeding step descriptors
+        const int w = tid / (2 * NSS), i = (tid / 2) % NSS, h = tid & 1;
+        S.sdesc[w][i][h] = seed_desc(a, S, S.sstep[w][i][h], T1);
       }
-      v16f sacc[DP / 32];
-#pragma unroll
-      for (int dt = 0; dt < DP / 32; ++dt) sacc[dt] = v16f{};
-      unsigned mcnt = 0;
-      // M-step slot tile of this wave (its own, or a distance owner's in narrow sweeps)
-      const int mt = __builtin_amdgcn_readfirstlane(static_cast<int>(S.mtile[wave]));
-      const int msl = 32 * mt + lr;
-      int mycl = -1, myit = 0;
-      if (mt >= 0 && msl < ncols) {
-        myit = max(static_cast<int>(S.sitem[msl]), 0);
-        mycl = S.scl[msl];
-      }
-      const bool mact = __ballot(mycl >= 0) != 0ull;  // wave-uniform: any running centre
-      // pipeline prologue: tile 0 in the ring, indices of tile 1
-      TileIdx<DP> nI;
-      {
-        TileIdx<DP> I0;
-        idx_issue<DP>(a, idx, 0, wave, lane, I0);
-        tile_dma<DP>(a, I0, ring, XN, wave, lane);
-        idx_issue<DP>(a, idx, RT, wave, lane, nI);
-        dma_wait();
-      }
-      unsigned pre[NSS];  // closest distances of the seeding steps of tile t-1 (loaded in t-1)
-#pragma unroll
-      for (int i = 0; i < NSS; ++i) pre[i] = 0;
+      const int hh = lane >> 5, lr = lane & 31;
 #ifdef CC_KM_STAMPS
       unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-      __syncthreads();
-      KM_STAMP(sw0);
-      KM_ACC(6, swp, sw0);
-      for (int t = 0; t <= T + 1; ++t) {
-        KM_STAMP(s0);
-        int tidl = tid;
-        asm volatile("" : "+v"(tidl));
-        // gather: rows of tile t+1 by LDS-DMA (indices loaded last iteration), indices of
-        // tile t+2; E-step operands of tile t (consumed next iteration)
-        if (t + 1 < T) tile_dma<DP>(a, nI, ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * 64, wave, lane);
-        if (t + 2 < T) idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
-        unsigned npre[NSS];
-        estep_prefetch<DP>(a, S, t, T, tidl, dbuf, T1, npre);
-        KM_STAMP(s1);
-        // Stagger: waves w and w+4 share a SIMD; w+4 runs its E-step (VALU) first so that one
-        // of the pair issues MFMAs while the other works on the vector pipe.
-        __builtin_amdgcn_sched_barrier(0);  // phases do not interleave: bounded working sets
-        if (wave >= 4) estep<DP>(a, S, t, T, tidl, Dt, Ls, XN, glab, dbuf, T1, pre, lw, nl, es);
-        __builtin_amdgcn_sched_barrier(0);
-        // distances of tile t (MFMA) -> D[t & 1]
-        if (tact && t < T) {
-          __builtin_amdgcn_s_setprio(1);  // MFMA-dense block first in the SIMD arbiter
-          const char* xs = ring + (t % NRING) * LY::SLOT;
-          v16f acc = {};
-          int lro = lr;
-          asm volatile("" : "+v"(lro));  // recompute the swizzled offsets (cheap) rather than hold 8
-          // B operands one k-step ahead of the MFMAs (bounded: 16 VGPRs in flight)
-          h8 bh = *reinterpret_cast<const h8*>(xs + xoff<DP>(lro, hh));
-          h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + xoff<DP>(lro, hh));
+      // Role-specialised waves, one of each role per SIMD.  Waves 0..NDW-1 gather the X tiles
+      // and run the distance MFMAs of slot tiles w and w + NDW; waves NDW..NW-1 run the E-steps
+      // dealt to them and the M-steps of slot tiles q and q + NDW (q = w - NDW).  Each role has
+      // its own loop (one barrier per tile in both), so their register sets never overlap and
+      // the vector chain of one role runs while the other role's MFMAs occupy the matrix pipe.
+      if (wave < NDW) {
+        const int nsub = __builtin_amdgcn_readfirstlane(static_cast<int>(32 * wave < ncols) +
+                                                        static_cast<int>(32 * (wave + NDW) < ncols));
+        h8 ah0[DP / 16], al0[DP / 16], ah1[DP / 16], al1[DP / 16];
+        slot_frags<DP>(a, S, cen, 32 * wave + lr, ncols, hh, ah0, al0);
+        slot_frags<DP>(a, S, cen, 32 * (wave + NDW) + lr, ncols, hh, ah1, al1);
+        // the distance wave's share of the E-steps (at most NLS_D Lloyd, NSS_D seeding steps)
+        EState<NLS_D, NSS_D> es;
 #pragma unroll
-          for (int s = 0; s < DP / 16; ++s) {
-            h8 nh = bh, nl = bl;
-            if (s + 1 < DP / 16) {
-              const int off = xoff<DP>(lro, 2 * (s + 1) + hh);
-              nh = *reinterpret_cast<const h8*>(xs + off);
-              nl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
-            }
-            acc = mfma16(ah[s], bl, acc);
-            acc = mfma16(al[s], bh, acc);
-            acc = mfma16(ah[s], bh, acc);
-            __builtin_amdgcn_sched_barrier(0);
-            bh = nh;
-            bl = nl;
-          }
-          float* drow = Dt + (t & 1) * (RT * DSD) + lr * DSD + 32 * ct + 4 * hh;
-          const float* cn = S.cnorm + 32 * ct + 4 * hh;
+        for (int i = 0; i < NLS_D; ++i) es.iaccL[i] = 0.f;
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {  // slots 8g + 4hh .. +3 of the tile: one b128 store
-            const float4 c4 = *reinterpret_cast<const float4*>(cn + 8 * g);
-            float4 d;
-            d.x = c4.x - a.dscale * acc[4 * g];
-            d.y = c4.y - a.dscale * acc[4 * g + 1];
-            d.z = c4.z - a.dscale * acc[4 * g + 2];
-            d.w = c4.w - a.dscale * acc[4 * g + 3];
-            *reinterpret_cast<float4*>(drow + 8 * g) = d;
-          }
-          __builtin_amdgcn_s_setprio(0);
-        }
-        KM_STAMP(s2);
-        __builtin_amdgcn_sched_barrier(0);
-        if (wave < 4) estep<DP>(a, S, t, T, tidl, Dt, Ls, XN, glab, dbuf, T1, pre, lw, nl, es);
-        __builtin_amdgcn_sched_barrier(0);
-        KM_STAMP(s3);
-        // M-step of tile t-2 (one-hot x X on f16 MFMA; counts by popcount)
-        if (mact && t >= 2) {
-          const int tm = t - 2;
-          const char* xs = ring + (tm % NRING) * LY::SLOT;
-          const uint8_t* lsb = Ls + (tm & 1) * (IMAX * RT) + myit * RT;
-          int lanel = lane;
-          asm volatile("" : "+v"(lanel));
-          const int G = lanel >> 4, q = (lanel >> 2) & 3, pp = lanel & 3;
+        for (int i = 0; i < NSS_D; ++i) es.iaccS[i] = 0.f;
+        const int nl = __builtin_amdgcn_readfirstlane(S.nlw[wave]);
+        const int ns = __builtin_amdgcn_readfirstlane(S.nsw[wave]);
+        unsigned lw[NLS_D];
 #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const unsigned long long lab8 = *reinterpret_cast<const unsigned long long*>(lsb + 16 * s2 + 8 * hh);
-            u32x4 ohu;
-            unsigned nb = 0;
+        for (int i = 0; i < NLS_D; ++i)
+          lw[i] = __builtin_amdgcn_readfirstlane(i < nl ? S.iw0[S.lstep[wave][i]] : 0u);
+        unsigned pre[NSS_D];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
-              const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
-              ohu[j] = ((b0 == mycl) ? 0x3C00u : 0u) | ((b1 == mycl) ? 0x3C000000u : 0u);
-              nb += (b0 == mycl) + (b1 == mycl);
-            }
-            mcnt += nb;
-            const h8 oh = __builtin_bit_cast(h8, ohu);
-            const int row0 = 16 * s2 + 8 * (G >> 1) + q;
-            // transposed B reads one feature block ahead of its MFMAs (the LDS latency of
-            // block dt+1 hides under block dt's two MFMAs)
-            auto rd = [&](int dt, s4 (&r)[4]) __attribute__((always_inline)) {
-              const int chn = 4 * dt + 2 * (G & 1) + (pp >> 1);
-              const int a0 = xoff<DP>(row0, chn) + 8 * (pp & 1);
-              const int a1 = xoff<DP>(row0 + 4, chn) + 8 * (pp & 1);
-              r[0] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a0));
-              r[1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + a1));
-              r[2] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a0));
-              r[3] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xs + LY::IMG + a1));
-            };
-            s4 rc[4], rn[4];
-            rd(0, rc);
-#pragma unroll
-            for (int dt = 0; dt < DP / 32; ++dt) {
-              if (dt + 1 < DP / 32) rd(dt + 1, rn);
-              const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(rc[0], rc[1], 0, 1, 2, 3, 4, 5, 6, 7));
-              const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(rc[2], rc[3], 0, 1, 2, 3, 4, 5, 6, 7));
-              sacc[dt] = mfma16(oh, bl, sacc[dt]);
-              sacc[dt] = mfma16(oh, bh, sacc[dt]);
-              __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-              for (int k = 0; k < 4; ++k) rc[k] = rn[k];
-            }
-          }
-        }
-        if ((t % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
-        KM_STAMP(s4);
-        // tile t+1 and the E-step operands have landed (this iteration's stores may still be
-        // in flight: one per Lloyd step, two per seeding step, issued after every load)
-        if (t >= 1 && t * RT <= m)  // tile t-1 full: every step issued its store instructions
-          dma_wait_leaving(__builtin_amdgcn_readfirstlane(S.nlw[wave]) + 2 * __builtin_amdgcn_readfirstlane(S.nsw[wave]));
-        else
+        for (int i = 0; i < NSS_D; ++i) pre[i] = 0;
+        // pipeline prologue: tile 0 in the ring, indices of tile 1
+        TileIdx<DP> nI;
+        {
+          TileIdx<DP> I0;
+          TileAddr<DP> A0;
+          idx_issue<DP>(a, idx, 0, wave, lane, I0);
+          tile_addr<DP>(a, I0, wave, lane, A0);
+          tile_issue<DP>(A0, ring, XN, wave);
+          idx_issue<DP>(a, idx, RT, wave, lane, nI);
           dma_wait();
-        KM_STAMP(s5);
-#pragma unroll
-        for (int i = 0; i < NSS; ++i) pre[i] = npre[i];
+          tile_addr_hold<DP>(A0);
+        }
         __syncthreads();
-        KM_STAMP(s6);
-        KM_ACC(0, s0, s1);
-        KM_ACC(1, s1, s2);
-        KM_ACC(2, s2, s3);
-        KM_ACC(3, s3, s4);
-        KM_ACC(4, s4, s5);
-        KM_ACC(5, s5, s6);
+        KM_STAMP(sw0);
+        KM_ACC(6, swp, sw0);
+        for (int t = 0; t <= T + 1; ++t) {
+          KM_STAMP(s0);
+          // rows of tile t+1 by LDS-DMA (indices loaded last iteration), indices of tile t+2
+          // addresses of t+1 (consuming the index registers), the index loads of t+2 into them,
+          // then the pieces: the compiler's own waits on the index registers all precede the DMA
+          // (both unconditional, so that no branch lets the compiler reorder them: past the end the
+          // index loads are clamped to row m-1 and unused)
+          TileAddr<DP> An;
+          tile_addr<DP>(a, nI, wave, lane, An);
+          idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
+          if (t + 1 < T) tile_issue<DP>(An, ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * 64, wave);
+          KM_STAMP(s1);
+          if (t < T) {  // distances of tile t (MFMA) -> D[t & 1]
+            const char* xs = ring + (t % NRING) * LY::SLOT;
+            float* dtile = Dt + (t & 1) * (RT * DSD);
+            if (nsub == 2)
+              dist_tiles<DP, 2>(a, S, xs, dtile, wave, lane, ah0, al0, ah1, al1);
+            else if (nsub == 1)
+              dist_tiles<DP, 1>(a, S, xs, dtile, wave, lane, ah0, al0, ah1, al1);
+          }
+          KM_STAMP(s2);
+          {
+            int tidl = tid;
+            asm volatile("" : "+v"(tidl));
+            unsigned npre[NSS_D];
+            estep_prefetch<NSS_D>(a, S, t, T, tidl, ns, dbuf, npre);
+            estep<DP, NLS_D, NSS_D>(a, S, t, T, tidl, Dt, Ls, XN, glab, dbuf, pre, lw, nl, ns, es);
+            if ((t % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
+#pragma unroll
+            for (int i = 0; i < NSS_D; ++i) pre[i] = npre[i];
+          }
+          KM_STAMP(s2e);
+          dma_wait();  // tile t+1 and the indices of t+2 have landed
+          tile_addr_hold<DP>(An);
+          KM_STAMP(s3);
+          __syncthreads();
+          KM_STAMP(s4);
+          KM_ACC(0, s0, s1);
+          KM_ACC(1, s1, s2);
+          KM_ACC(2, s2, s2e);
+          KM_ACC(4, s2e, s3);
+          KM_ACC(5, s3, s4);
+        }
+        estep_flush(S, tid, es);
+      } else {
+        const int q = wave - NDW;
+        EState<NLS, NSS> es;
+#pragma unroll
+        for (int i = 0; i < NLS; ++i) es.iaccL[i] = 0.f;
+#pragma unroll
+        for (int i = 0; i < NSS; ++i) es.iaccS[i] = 0.f;
+        // this wave's Lloyd step words, wave-uniform for the whole sweep
+        const int nl = __builtin_amdgcn_readfirstlane(S.nlw[wave]);
+        const int ns = __builtin_amdgcn_readfirstlane(S.nsw[wave]);
+        unsigned lw[NLS];
+#pragma unroll
+        for (int i = 0; i < NLS; ++i)
+          lw[i] = __builtin_amdgcn_readfirstlane(i < nl ? S.iw0[S.lstep[wave][i]] : 0u);
+        // M-step slot tiles q and q + NDW: the lane's slot, its cluster and item
+        const int msl0 = 32 * q + lr, msl1 = 32 * (q + NDW) + lr;
+        int mycl0 = -1, myit0 = 0, mycl1 = -1, myit1 = 0;
+        // (myit: the problem whose M-step labels the lane's slot reads; 0 when the slot is idle)
+        if (msl0 < ncols) {
+          mycl0 = S.scl[msl0];
+          if (mycl0 >= 0) myit0 = S.iprob[S.sitem[msl0]];
+        }
+        if (msl1 < ncols) {
+          mycl1 = S.scl[msl1];
+          if (mycl1 >= 0) myit1 = S.iprob[S.sitem[msl1]];
+        }
+        const bool mact0 = __ballot(mycl0 >= 0) != 0ull;  // wave-uniform: any running centre
+        const bool mact1 = __ballot(mycl1 >= 0) != 0ull;
+        v16f sacc0[DP / 32], sacc1[DP / 32];
+#pragma unroll
+        for (int dt = 0; dt < DP / 32; ++dt) sacc0[dt] = sacc1[dt] = v16f{};
+        unsigned mcnt0 = 0, mcnt1 = 0;
+        unsigned pre[NSS];  // closest distances of the seeding steps of tile t-1 (loaded in t-1)
+#pragma unroll
+        for (int i = 0; i < NSS; ++i) pre[i] = 0;
+        __syncthreads();
+        KM_STAMP(sw0);
+        KM_ACC(6, swp, sw0);
+        for (int t = 0; t <= T + 1; ++t) {
+          KM_STAMP(s0);
+          int tidl = tid;
+          asm volatile("" : "+v"(tidl));
+          // E-step operands of tile t (consumed next iteration)
+          unsigned npre[NSS];
+          estep_prefetch<NSS>(a, S, t, T, tidl, ns, dbuf, npre);
+          KM_STAMP(s1);
+          estep<DP, NLS, NSS>(a, S, t, T, tidl, Dt, Ls, XN, glab, dbuf, pre, lw, nl, ns, es);
+          KM_STAMP(s2);
+          // M-steps of tile t-2 (one-hot x X on f16 MFMA; counts by popcount)
+          if (t >= 2) {
+            const int tm = t - 2;
+            const char* xs = ring + (tm % NRING) * LY::SLOT;
+            const uint8_t* lsb = Ls + (tm & 1) * (IMAX * RT);
+            if (mact0 || mact1)  // both tiles share the transposed X reads (a tile without running
+                                 // centres has an all-zero one-hot)
+              mstep_tiles<DP, 2>(xs, lsb + myit0 * RT, lsb + myit1 * RT, lane, mycl0, mycl1, sacc0, sacc1, mcnt0, mcnt1);
+          }
+          if ((t % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
+          KM_STAMP(s3);
+#pragma unroll
+          for (int i = 0; i < NSS; ++i) pre[i] = npre[i];
+          __syncthreads();
+          KM_STAMP(s4);
+          KM_ACC(0, s0, s1);
+          KM_ACC(2, s1, s2);
+          KM_ACC(3, s2, s3);
+          KM_ACC(5, s3, s4);
+        }
+        estep_flush(S, tid, es);
+        dma_wait();  // label and closest-distance stores land before the post-sweep reads
+        // sums -> Sm (aliases the ring and D: every reader passed the last loop barrier); counts
+        if (mact0) msum_out<DP>(a, S, Sm, sacc0, mcnt0, q, msl0, lr, hh);
+        if (mact1) msum_out<DP>(a, S, Sm, sacc1, mcnt1, q + NDW, msl1, lr, hh);
       }
 #ifdef CC_KM_STAMPS
 #ifdef CC_KM_STAMPS_NARROW
@@ -1164,19 +1291,6 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
 #endif
         for (int k = 0; k < 7; ++k) atomicAdd(&a.stats[8 + 8 * wave + k], st_acc[k]);
 #endif
-      estep_flush(S, tid, es);
-      // sums -> Sm (aliases the ring and D: every reader passed the last barrier); counts
-      if (mact) {
-#pragma unroll
-        for (int dt = 0; dt < DP / 32; ++dt)
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int s2 = 32 * mt + (v & 3) + 8 * (v >> 2) + 4 * hh;
-            Sm[s2 * DP + 32 * dt + lr] = sacc[dt][v] * a.inv_scale;
-          }
-        const unsigned tot = mcnt + __shfl_xor(mcnt, 32);
-        if (hh == 0) S.cnt[msl] = tot;
-      }
       __syncthreads();
 
       KM_STAMP(pp0);
@@ -1617,6 +1731,10 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
   const int nh = h_end - h_begin;
   if (nh == 0) return CC_OK;
   const WsLayout L = ws_layout(m, dpad, units_host, nU, seedmax);
+  if (static_cast<double>(seedmax) * (L.Tws + 1) * ((m + 63) & ~63) >= 4294967296.0) {
+    cc::set_error("cc_kmeans_batched: closest-distance buffers exceed 2^32 floats (lower seedmax)");
+    return CC_ERR_UNSUPPORTED;
+  }
   if (!workspace || ws_bytes < WS_HEADER + L.per_wg * static_cast<size_t>(grid)) {
     cc::set_error("cc_kmeans_batched: workspace too small");
     return CC_ERR_ARG;
