@@ -278,11 +278,11 @@ __device__ __forceinline__ void idx_issue(const KArgs& a, const int32_t* idx, in
                                           TileIdx<DP>& I) {
   using GA = Gather<DP>;
 #pragma unroll
-  for (int j = 0; j < GA::PER; ++j) {
-    const int k = wave + NDW * j;
-    const int B = 1024 * k + 16 * lane;
-    const int off = B % GA::IMG;
-    I.src[j] = idx[min(r0 + off / GA::ROWB, a.m - 1)];
+  for (int j = 0; j < GA::PER; ++j) {  // unsigned: the divisions by powers of two are shifts
+    const unsigned k = wave + NDW * j;
+    const unsigned B = 1024u * k + 16u * static_cast<unsigned>(lane);
+    const unsigned off = B % GA::IMG;
+    I.src[j] = idx[min(r0 + static_cast<int>(off / GA::ROWB), a.m - 1)];
   }
   I.xsrc = idx[min(r0 + lane, a.m - 1)];
 }
@@ -319,14 +319,14 @@ __device__ __forceinline__ void tile_addr(const KArgs& a, const TileIdx<DP>& I, 
   int ln = lane;
   asm volatile("" : "+v"(ln));  // recompute the per-lane chunk offsets (cheap) rather than hold them
 #pragma unroll
-  for (int j = 0; j < GA::PER; ++j) {
-    const int k = wave + NDW * j;
-    const int B = 1024 * k + 16 * ln;
-    const int part = B / GA::IMG, off = B - part * GA::IMG;
-    const int row = off / GA::ROWB, ch = ((off % GA::ROWB) >> 4) ^ xsw<DP>(row);
-    A.src[j] = a.Xhl + static_cast<size_t>(I.src[j]) * (2 * DP) + part * DP + 8 * ch;
+  for (int j = 0; j < GA::PER; ++j) {  // unsigned: the divisions by powers of two are shifts
+    const unsigned k = wave + NDW * j;
+    const unsigned B = 1024u * k + 16u * static_cast<unsigned>(ln);
+    const unsigned part = B / GA::IMG, off = B % GA::IMG;
+    const unsigned row = off / GA::ROWB, ch = ((off % GA::ROWB) >> 4) ^ static_cast<unsigned>(xsw<DP>(static_cast<int>(row)));
+    A.src[j] = a.Xhl + static_cast<size_t>(static_cast<unsigned>(I.src[j])) * (2 * DP) + (part * DP + 8u * ch);
   }
-  A.xsrc = a.xnorm + I.xsrc;
+  A.xsrc = a.xnorm + static_cast<unsigned>(I.xsrc);
 }
 
 // Keeps the pieces' address registers allocated up to this point (after the end-of-iteration
@@ -790,18 +790,26 @@ __device__ __forceinline__ void dist_tiles(const KArgs& a, const State& S, const
 
 // E/M wave: one-hot A operand of the lane's slot (cluster mycl) for 8 rows of its 16-row k-block
 // s2 of a tile (f16 1.0 where label == mycl), and their count.
+// Packed: per 4 labels, XOR with the cluster replicated in every byte, a carry-free zero-byte
+// test (0x80 where the label matches), the flags scaled to 0x3C (f16 1.0 = 0x3C00) and placed
+// into the high byte of each f16 by v_perm; the count is a popcount of the flags.  A cluster of
+// -1 (no running centre) compares against 0xFE, which no label takes (labels are < 127, 0xFF
+// marks rows past m).
 __device__ __forceinline__ h8 onehot8(const uint8_t* lsb, int s2, int hh, int mycl, unsigned& mcnt) {
-  const unsigned long long lab8 = *reinterpret_cast<const unsigned long long*>(lsb + 16 * s2 + 8 * hh);
+  const uint2 lab = *reinterpret_cast<const uint2*>(lsb + 16 * s2 + 8 * hh);
+  const unsigned rep = static_cast<unsigned>(mycl < 0 ? 0xFE : mycl) * 0x01010101u;
   u32x4 ohu;
-  unsigned nb = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int b0 = static_cast<int>((lab8 >> (16 * j)) & 0xFFu);
-    const int b1 = static_cast<int>((lab8 >> (16 * j + 8)) & 0xFFu);
-    ohu[j] = ((b0 == mycl) ? 0x3C00u : 0u) | ((b1 == mycl) ? 0x3C000000u : 0u);
-    nb += (b0 == mycl) + (b1 == mycl);
+  for (int h = 0; h < 2; ++h) {
+    const unsigned y = (h ? lab.y : lab.x) ^ rep;
+    const unsigned z = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;  // 0x80: byte == 0
+    mcnt += __builtin_popcount(z);
+    const unsigned t = z >> 7;               // 0 / 1 per byte
+    const unsigned f = (t << 6) - (t << 2);  // 0 / 0x3C per byte (no borrow across bytes)
+    // f16 pairs: label 2i -> bits 15:8 of dword i, label 2i+1 -> bits 31:24 (selector 12 = 0x00)
+    ohu[2 * h] = __builtin_amdgcn_perm(0u, f, 0x010C000Cu);
+    ohu[2 * h + 1] = __builtin_amdgcn_perm(0u, f, 0x030C020Cu);
   }
-  mcnt += nb;
   return __builtin_bit_cast(h8, ohu);
 }
 
@@ -1167,16 +1175,6 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         KM_ACC(6, swp, sw0);
         for (int t = 0; t <= T + 1; ++t) {
           KM_STAMP(s0);
-          // rows of tile t+1 by LDS-DMA (indices loaded last iteration), indices of tile t+2
-          // addresses of t+1 (consuming the index registers), the index loads of t+2 into them,
-          // then the pieces: the compiler's own waits on the index registers all precede the DMA
-          // (both unconditional, so that no branch lets the compiler reorder them: past the end the
-          // index loads are clamped to row m-1 and unused)
-          TileAddr<DP> An;
-          tile_addr<DP>(a, nI, wave, lane, An);
-          idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
-          if (t + 1 < T) tile_issue<DP>(An, ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * 64, wave);
-          KM_STAMP(s1);
           if (t < T) {  // distances of tile t (MFMA) -> D[t & 1]
             const char* xs = ring + (t % NRING) * LY::SLOT;
             float* dtile = Dt + (t & 1) * (RT * DSD);
@@ -1185,6 +1183,17 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
             else if (nsub == 1)
               dist_tiles<DP, 1>(a, S, xs, dtile, wave, lane, ah0, al0, ah1, al1);
           }
+          KM_STAMP(s1);
+          // rows of tile t+1 by LDS-DMA, after the distance MFMAs so that the pieces' address
+          // registers (held to the end-of-iteration wait) do not overlap the A fragments'
+          // busiest stretch: addresses of t+1 (consuming the index registers loaded last
+          // iteration), the index loads of t+2 into them, then the pieces (all unconditional
+          // but the pieces, so no branch lets the compiler reorder them; past the end the index
+          // loads are clamped to row m-1 and unused).  The pieces land under the E-step share.
+          TileAddr<DP> An;
+          tile_addr<DP>(a, nI, wave, lane, An);
+          idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
+          if (t + 1 < T) tile_issue<DP>(An, ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * 64, wave);
           KM_STAMP(s2);
           {
             int tidl = tid;
@@ -1202,8 +1211,8 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           KM_STAMP(s3);
           __syncthreads();
           KM_STAMP(s4);
-          KM_ACC(0, s0, s1);
-          KM_ACC(1, s1, s2);
+          KM_ACC(1, s0, s1);
+          KM_ACC(0, s1, s2);
           KM_ACC(2, s2, s2e);
           KM_ACC(4, s2e, s3);
           KM_ACC(5, s3, s4);
