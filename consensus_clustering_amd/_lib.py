@@ -24,6 +24,8 @@ SIGNATURES = {
     "cc_version": (ctypes.c_char_p, []),
     "cc_last_error": (ctypes.c_char_p, []),
     "cc_resample_indices": (_c_int, [_c_u32, _c_int, _c_int, _c_int, _c_int, _vp, _c_int]),
+    "cc_resample_device_max_n": (_c_int, []),
+    "cc_resample_device": (_c_int, [_c_u32, _c_int, _c_int, _c_int, _c_int, _vp, _vp]),
     "cc_random_sample": (_c_int, [_c_u32, _c_i64, _vp]),
     "cc_num_tiles": (_c_i64, [_c_int]),
     "cc_scatter_labels": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),

@@ -7,7 +7,8 @@ when n_iterations < 256 else uint16 (CC.py:107), cij float32 with a unit diagona
 bin_edges float32, hist/cdf float64, pac_area np.float64.
 
 What runs where (``fit``):
-  resampling      host-native numpy-RandomState replay (libccmi cc_resample_indices)
+  resampling      numpy-RandomState replay on the device (libccmi cc_resample_device, n <= 65536)
+                  or on host threads (cc_resample_indices)
   clustering      default clusterer (KMeans) -> all (h, K, init) problems in batched
                   gfx950 launches (cc_kmeans_batched); any other plugin clusterer
                   (e.g. GaussianMixture) keeps the reference's host fit_predict per
@@ -81,6 +82,7 @@ class ConsensusClustering:
         device=None,
         workspace_budget=8 << 30,
         precision='auto',
+        resampling='auto',
     ):
         self.K_range = K_range
         self.n_iterations = n_iterations
@@ -104,6 +106,9 @@ class ConsensusClustering:
         # k-means arithmetic: 'f64' = float64 like sklearn on float64 input (cc_kmeans_f64),
         # 'fast' = the float32-class f16 hi/lo MFMA engine; 'auto' picks by the input dtype
         self.precision = precision
+        # where the resample indices are drawn: 'device' (cc_resample_device, n <= 65536),
+        # 'host' (native threads, then uploaded), 'auto' = device when n allows; identical draws
+        self.resampling = resampling
         self.timings_ = {}
         self._rehearsal = None  # (rank, world): bench tooling only, see fit()
 
@@ -172,18 +177,32 @@ class ConsensusClustering:
         # outside the shard stay zero and are never read (the co-sampling counts come from the
         # merged label matrix, not from the indices)
         h0, h1 = dist.shard(H, rank, W)
-        own = engine.resample_indices(self.random_state, n, m, h0, h1) if h1 > h0 else None
-        if (h0, h1) == (0, H):
-            idx = own
-            idx_d = torch.from_numpy(idx).to(dev)
+        if self.resampling not in ('auto', 'device', 'host'):
+            raise ValueError("resampling must be 'auto', 'device' or 'host'")
+        on_dev = self.resampling != 'host' and n <= engine.resample_device_max_n()
+        if self.resampling == 'device' and not on_dev:
+            raise ValueError(f"resampling='device' needs n <= {engine.resample_device_max_n()}")
+        self.resampling_ = 'device' if on_dev else 'host'
+        idx = None  # host copy, made only when a host consumer needs it (resampling_indices_)
+        if on_dev:
+            idx_d = (torch.empty if (h0, h1) == (0, H) else torch.zeros)((H, m), dtype=torch.int32, device=dev)
+            if h1 > h0:
+                engine.resample_indices_device(self.random_state, n, m, h0, h1, dev, out=idx_d[h0:h1])
         else:
-            idx = np.zeros((H, m), dtype=np.int32)
-            idx_d = torch.zeros((H, m), dtype=torch.int32, device=dev)
-            if own is not None:
-                idx[h0:h1] = own
-                idx_d[h0:h1] = torch.from_numpy(own).to(dev)
+            own = engine.resample_indices(self.random_state, n, m, h0, h1) if h1 > h0 else None
+            if (h0, h1) == (0, H):
+                idx = own
+                idx_d = torch.from_numpy(idx).to(dev)
+            else:
+                idx = np.zeros((H, m), dtype=np.int32)
+                idx_d = torch.zeros((H, m), dtype=torch.int32, device=dev)
+                if own is not None:
+                    idx[h0:h1] = own
+                    idx_d[h0:h1] = torch.from_numpy(own).to(dev)
         Hpad = engine.pad_h(H)
         labels = engine.new_label_matrix(max(len(Ks), 1), n, Hpad, dev)
+        if on_dev:
+            torch.cuda.synchronize(dev)  # stage timing only: the k-means waits for the indices anyway
         t_rs = time.perf_counter()
 
         km = self._kmeans_params()
@@ -216,6 +235,8 @@ class ConsensusClustering:
         elif Ks:
             if isinstance(X, torch.Tensor):
                 X = X.cpu().numpy()
+            if idx is None:
+                idx = idx_d.cpu().numpy()
             for k, K in enumerate(Ks):
                 self._K = K
                 self._set_clusterer_K()
@@ -264,7 +285,7 @@ class ConsensusClustering:
                 res['mij'] = res['iij'] = res['cij'] = None
             self.cdf_at_K_data[K] = res
         self.pair_counts_ = {K: counts_h[k] for k, K in enumerate(Ks)}
-        self.resampling_indices_ = idx  # rows [h0, h1) of this rank (all of them at W = 1)
+        self._idx_host, self._idx_dev = idx, idx_d  # rows [h0, h1) of this rank (all at W = 1)
         self.resample_range_ = (h0, h1)
         self.labels_ = labels  # device uint8 [nK, n, Hpad]; 0xFF = not sampled
         self._finish_selection()
@@ -378,6 +399,14 @@ class ConsensusClustering:
         agg = AgglomerativeClustering(n_clusters=K, metric='precomputed',
                                       linkage=self.agg_clustering_linkage)
         return agg.fit_predict(D)
+
+    @property
+    def resampling_indices_(self):
+        """int32 [H, m] host copy of the resample indices (rows [h0, h1) of this rank; copied
+        from the device on first access when they were drawn there)."""
+        if getattr(self, '_idx_host', None) is None and getattr(self, '_idx_dev', None) is not None:
+            self._idx_host = self._idx_dev.cpu().numpy()
+        return getattr(self, '_idx_host', None)
 
     def _plot_cdf(self, ax=None):
         """Consensus CDF per K as a step curve over the bin upper edges, with the PAC interval

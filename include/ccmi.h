@@ -12,6 +12,7 @@
  * (/root/reference/consensus_clustering_parallelised.py, "CC.py" below):
  *
  *   cc_resample_indices   CC.py:216-241  _get_subsampling_indices (numpy RandomState replay)
+ *   cc_resample_device    the same on the device (n <= 65536), straight into HBM
  *   cc_scatter_labels     CC.py:260-262, :284-285  indicator / one-hot row placement
  *   cc_cosample           CC.py:264  I = S^T S            (int8 MFMA, upper-triangle tiles)
  *   cc_coassoc            CC.py:287-290 + :338-344  M += L^T L fused with the 20-bin histogram
@@ -68,6 +69,14 @@ int cc_random_sample(uint32_t seed, int64_t count, double* out);
 int64_t cc_num_tiles(int n);
 
 /* ---- device kernels ----------------------------------------------------- */
+
+/* cc_resample_indices on the device (CC.py:231-239): out [h_end-h_begin][m] int32 in device
+ * memory, bit-identical to numpy.random.RandomState(seed + h).permutation(n)[:m].  One
+ * workgroup per resample (Fisher-Yates over a uint16 array in LDS), so 1 <= n <=
+ * cc_resample_device_max_n() (65536); larger n stays on the host replay. */
+int cc_resample_device_max_n(void);
+int cc_resample_device(uint32_t seed, int h_begin, int h_end, int n, int m, int32_t* out,
+                       void* stream);
 
 /* labels_nh[idx[h][r] * ldl + h] = labels_hm ? labels_hm[h*m + r] : 0 for h < H, r < m.
  * labels_nh must be pre-filled with 0xFF (= not sampled).  (CC.py:260-262, :284-285) */
