@@ -622,6 +622,24 @@ __device__ __forceinline__ void amin16(const float4 (&v)[4], const int (&col)[4]
   if (bv[0] < best) { best = bv[0]; lab = bi[0]; }
 }
 
+// The same over 2 chunks (8 slots): items with K <= 16 hold at most 2 chunks per half-wave.
+__device__ __forceinline__ void amin8(const float4 (&v)[2], const int (&col)[2], float& best, int& lab) {
+  float bv[2];
+  int bi[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float m0 = v[u].x, m1 = v[u].z;
+    int i0 = col[u], i1 = col[u] + 2;
+    if (v[u].y < m0) { m0 = v[u].y; i0 = col[u] + 1; }
+    if (v[u].w < m1) { m1 = v[u].w; i1 = col[u] + 3; }
+    if (m1 < m0) { m0 = m1; i0 = i1; }
+    bv[u] = m0;
+    bi[u] = i0;
+  }
+  if (bv[1] < bv[0]) { bv[0] = bv[1]; bi[0] = bi[1]; }
+  if (bv[0] < best) { best = bv[0]; lab = bi[0]; }
+}
+
 template <int DP, int NL, int NS>
 __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int T, int tidl, const float* Dt,
                                       uint8_t* Ls, const float* XN, uint8_t* glab, float* dbuf,
@@ -670,15 +688,26 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
     const int base = off + (hh ? 4 * h0 : 0), cnt = hh ? C - h0 : h0;
     float best = INF;
     int lab = 0;
-    for (int j0 = 0; j0 < h0; j0 += 4) {  // 4 chunk reads in flight, then a tree argmin
-      int col[4];
-      float4 v[4];
+    if (h0 <= 2) {  // wave-uniform: K <= 16, at most 2 chunks per half-wave
+      int col[2];
+      float4 v[2];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        col[u] = (j0 + u < cnt) ? base + 4 * (j0 + u) : CW;  // CW..CW+3 hold +inf
+      for (int u = 0; u < 2; ++u) {
+        col[u] = (u < cnt) ? base + 4 * u : CW;  // CW..CW+3 hold +inf
         v[u] = *reinterpret_cast<const float4*>(drow + col[u]);
       }
-      amin16(v, col, best, lab);
+      amin8(v, col, best, lab);
+    } else {
+      for (int j0 = 0; j0 < h0; j0 += 4) {  // 4 chunk reads in flight, then a tree argmin
+        int col[4];
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          col[u] = (j0 + u < cnt) ? base + 4 * (j0 + u) : CW;  // CW..CW+3 hold +inf
+          v[u] = *reinterpret_cast<const float4*>(drow + col[u]);
+        }
+        amin16(v, col, best, lab);
+      }
     }
     // merge the halves (v_permlane32_swap: lane i <-> i^32 without LDS): lower value, ties to
     // the lower slot (half 0 holds the lower slots)
