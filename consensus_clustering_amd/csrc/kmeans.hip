@@ -601,13 +601,15 @@ __device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, i
   }
 }
 
-// strict-< argmin of 4 aligned chunks (16 slots, columns col[u] .. col[u] + 3, increasing in u)
-// as a tree (dependency depth 4 instead of 16): ties keep the lower slot at every level.
-__device__ __forceinline__ void amin16(const float4 (&v)[4], const int (&col)[4], float& best, int& lab) {
-  float bv[4];
-  int bi[4];
+// strict-< argmin of NCH aligned chunks (4 slots each, columns col[u] .. col[u] + 3, increasing
+// in u) as a tree (dependency depth 2 + log2 NCH instead of 4 NCH): ties keep the lower slot at
+// every level.
+template <int NCH>
+__device__ __forceinline__ void amin_chunks(const float4 (&v)[NCH], const int (&col)[NCH], float& best, int& lab) {
+  float bv[NCH];
+  int bi[NCH];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < NCH; ++u) {
     float m0 = v[u].x, m1 = v[u].z;
     int i0 = col[u], i1 = col[u] + 2;
     if (v[u].y < m0) { m0 = v[u].y; i0 = col[u] + 1; }
@@ -616,28 +618,26 @@ __device__ __forceinline__ void amin16(const float4 (&v)[4], const int (&col)[4]
     bv[u] = m0;
     bi[u] = i0;
   }
-  if (bv[1] < bv[0]) { bv[0] = bv[1]; bi[0] = bi[1]; }
-  if (bv[3] < bv[2]) { bv[2] = bv[3]; bi[2] = bi[3]; }
-  if (bv[2] < bv[0]) { bv[0] = bv[2]; bi[0] = bi[2]; }
+#pragma unroll
+  for (int st = 1; st < NCH; st *= 2)
+#pragma unroll
+    for (int u = 0; u + st < NCH; u += 2 * st)
+      if (bv[u + st] < bv[u]) { bv[u] = bv[u + st]; bi[u] = bi[u + st]; }
   if (bv[0] < best) { best = bv[0]; lab = bi[0]; }
 }
 
-// The same over 2 chunks (8 slots): items with K <= 16 hold at most 2 chunks per half-wave.
-__device__ __forceinline__ void amin8(const float4 (&v)[2], const int (&col)[2], float& best, int& lab) {
-  float bv[2];
-  int bi[2];
+// Lloyd argmin of one half-wave over chunks j0 .. j0 + NCH - 1 (those at or past cnt read the
+// +inf columns CW..CW+3).
+template <int NCH>
+__device__ __forceinline__ void amin_half(const float* drow, int base, int j0, int cnt, float& best, int& lab) {
+  int col[NCH];
+  float4 v[NCH];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    float m0 = v[u].x, m1 = v[u].z;
-    int i0 = col[u], i1 = col[u] + 2;
-    if (v[u].y < m0) { m0 = v[u].y; i0 = col[u] + 1; }
-    if (v[u].w < m1) { m1 = v[u].w; i1 = col[u] + 3; }
-    if (m1 < m0) { m0 = m1; i0 = i1; }
-    bv[u] = m0;
-    bi[u] = i0;
+  for (int u = 0; u < NCH; ++u) {
+    col[u] = (j0 + u < cnt) ? base + 4 * (j0 + u) : CW;
+    v[u] = *reinterpret_cast<const float4*>(drow + col[u]);
   }
-  if (bv[1] < bv[0]) { bv[0] = bv[1]; bi[0] = bi[1]; }
-  if (bv[0] < best) { best = bv[0]; lab = bi[0]; }
+  amin_chunks<NCH>(v, col, best, lab);
 }
 
 template <int DP, int NL, int NS>
@@ -688,26 +688,13 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
     const int base = off + (hh ? 4 * h0 : 0), cnt = hh ? C - h0 : h0;
     float best = INF;
     int lab = 0;
-    if (h0 <= 2) {  // wave-uniform: K <= 16, at most 2 chunks per half-wave
-      int col[2];
-      float4 v[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        col[u] = (u < cnt) ? base + 4 * u : CW;  // CW..CW+3 hold +inf
-        v[u] = *reinterpret_cast<const float4*>(drow + col[u]);
-      }
-      amin8(v, col, best, lab);
+    // wave-uniform (one item per wave): the item's chunk count per half-wave
+    if (h0 <= 2) {
+      amin_half<2>(drow, base, 0, cnt, best, lab);
+    } else if (h0 <= 3) {
+      amin_half<3>(drow, base, 0, cnt, best, lab);
     } else {
-      for (int j0 = 0; j0 < h0; j0 += 4) {  // 4 chunk reads in flight, then a tree argmin
-        int col[4];
-        float4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          col[u] = (j0 + u < cnt) ? base + 4 * (j0 + u) : CW;  // CW..CW+3 hold +inf
-          v[u] = *reinterpret_cast<const float4*>(drow + col[u]);
-        }
-        amin16(v, col, best, lab);
-      }
+      for (int j0 = 0; j0 < h0; j0 += 4) amin_half<4>(drow, base, j0, cnt, best, lab);  // 4 reads in flight
     }
     // merge the halves (v_permlane32_swap: lane i <-> i^32 without LDS): lower value, ties to
     // the lower slot (half 0 holds the lower slots)
