@@ -832,11 +832,13 @@ __device__ __forceinline__ h8 onehot8(const uint8_t* lsb, int s2, int hh, int my
 // E/M wave: M-step of NS slot tiles over one X tile: sums += one-hot(labels == cluster of the
 // lane's slot) x (xh + xl) on f16 MFMA, counts by popcount.  B is the X tile read back
 // transposed with ds_read_b64_tr_b16 from the swizzled image, once for the NS tiles.
-// lsb0 / lsb1: the labels of the problem each tile's lane slot belongs to.
+// lsb0 / lsb1: the labels of the problem each tile's lane slot belongs to.  act1 (wave-uniform):
+// the second tile has a running centre; without one its MFMAs are skipped (narrow sweeps; d = 128
+// only).
 template <int DP, int NS>
 __device__ __forceinline__ void mstep_tiles(const char* xs, const uint8_t* lsb0, const uint8_t* lsb1, int lane,
                                             int mycl0, int mycl1, v16f (&sacc0)[DP / 32], v16f (&sacc1)[DP / 32],
-                                            unsigned& mcnt0, unsigned& mcnt1) {
+                                            unsigned& mcnt0, unsigned& mcnt1, bool act1) {
   using LY = Lay<DP>;
   int lanel = lane;
   asm volatile("" : "+v"(lanel));
@@ -866,9 +868,12 @@ __device__ __forceinline__ void mstep_tiles(const char* xs, const uint8_t* lsb0,
       const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(rc[0], rc[1], 0, 1, 2, 3, 4, 5, 6, 7));
       const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(rc[2], rc[3], 0, 1, 2, 3, 4, 5, 6, 7));
       sacc0[dt] = mfma16(oh0, bl, sacc0[dt]);
-      if constexpr (NS == 2) sacc1[dt] = mfma16(oh1, bl, sacc1[dt]);
+      if constexpr (NS == 2)
+        if (DP < 128 || act1) {  // the skip costs spills at d = 32 / 64 (C2 +7 %, C5 +3 %)
+          sacc1[dt] = mfma16(oh1, bl, sacc1[dt]);
+          sacc1[dt] = mfma16(oh1, bh, sacc1[dt]);
+        }
       sacc0[dt] = mfma16(oh0, bh, sacc0[dt]);
-      if constexpr (NS == 2) sacc1[dt] = mfma16(oh1, bh, sacc1[dt]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) rc[k] = rn[k];
@@ -1289,7 +1294,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
             const uint8_t* lsb = Ls + (tm & 1) * (IMAX * RT);
             if (mact0 || mact1)  // both tiles share the transposed X reads (a tile without running
                                  // centres has an all-zero one-hot)
-              mstep_tiles<DP, 2>(xs, lsb + myit0 * RT, lsb + myit1 * RT, lane, mycl0, mycl1, sacc0, sacc1, mcnt0, mcnt1);
+              mstep_tiles<DP, 2>(xs, lsb + myit0 * RT, lsb + myit1 * RT, lane, mycl0, mycl1, sacc0, sacc1, mcnt0, mcnt1, mact1);
           }
           if ((t % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
           KM_STAMP(s3);
