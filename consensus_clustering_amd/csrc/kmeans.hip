@@ -559,6 +559,12 @@ struct EState {
 };
 constexpr int FLUSH = 32;  // tiles per f32 partial
 
+// The first slot tile whose M-step E/M wave NDW + q runs (then + NDW).  Waves w and w + NDW
+// share a SIMD, so the M-step of slot tile q runs on another SIMD than its distance MFMAs
+// (wave q): in a narrow sweep (one slot tile) the two MFMA blocks use two matrix pipes.
+__host__ __device__ constexpr int mstep_tile(int q) { return (q + 1) % NDW; }
+static_assert(NEW == NDW, "one E/M wave per distance wave");
+
 __device__ __forceinline__ int iw_off(unsigned w) { return w & 0xFF; }
 __device__ __forceinline__ int iw_K(unsigned w) { return (w >> 8) & 0xFF; }
 __device__ __forceinline__ int iw_prob(unsigned w) { return (w >> 16) & 0x3F; }
@@ -763,26 +769,32 @@ __device__ __forceinline__ void dist_tiles(const KArgs& a, const State& S, const
   int lno = lane;
   asm volatile("" : "+v"(lno));  // per-lane offsets recomputed here (cheap), never held or spilled
   const int lro = lno & 31, hh = lno >> 5;
-  // B operands one k-step ahead of the MFMAs (bounded: 16 VGPRs in flight)
-  h8 bh = *reinterpret_cast<const h8*>(xs + xoff<DP>(lro, hh));
-  h8 bl = *reinterpret_cast<const h8*>(xs + LY::IMG + xoff<DP>(lro, hh));
+  // B operands PD k-steps ahead of the MFMAs.  Two slot tiles: one step (6 MFMAs cover the
+  // read; 16 VGPRs in flight).  One slot tile (narrow sweeps, where this wave's chain sets the
+  // tile time): three MFMAs per step do not cover an LDS read under DMA traffic, so three steps
+  // ahead, in the registers the second accumulator leaves free.
+  constexpr int KS = DP / 16, PD = NS == 1 ? 2 : 1;
+  h8 bh[KS], bl[KS];
 #pragma unroll
-  for (int s = 0; s < DP / 16; ++s) {
-    h8 nh = bh, nl = bl;
-    if (s + 1 < DP / 16) {
-      const int off = xoff<DP>(lro, 2 * (s + 1) + hh);
-      nh = *reinterpret_cast<const h8*>(xs + off);
-      nl = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
+  for (int s = 0; s < PD && s < KS; ++s) {
+    const int off = xoff<DP>(lro, 2 * s + hh);
+    bh[s] = *reinterpret_cast<const h8*>(xs + off);
+    bl[s] = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + PD < KS) {
+      const int off = xoff<DP>(lro, 2 * (s + PD) + hh);
+      bh[s + PD] = *reinterpret_cast<const h8*>(xs + off);
+      bl[s + PD] = *reinterpret_cast<const h8*>(xs + LY::IMG + off);
     }
-    acc0 = mfma16(ah0[s], bl, acc0);
-    if constexpr (NS == 2) acc1 = mfma16(ah1[s], bl, acc1);
-    acc0 = mfma16(al0[s], bh, acc0);
-    if constexpr (NS == 2) acc1 = mfma16(al1[s], bh, acc1);
-    acc0 = mfma16(ah0[s], bh, acc0);
-    if constexpr (NS == 2) acc1 = mfma16(ah1[s], bh, acc1);
+    acc0 = mfma16(ah0[s], bl[s], acc0);
+    if constexpr (NS == 2) acc1 = mfma16(ah1[s], bl[s], acc1);
+    acc0 = mfma16(al0[s], bh[s], acc0);
+    if constexpr (NS == 2) acc1 = mfma16(al1[s], bh[s], acc1);
+    acc0 = mfma16(ah0[s], bh[s], acc0);
+    if constexpr (NS == 2) acc1 = mfma16(ah1[s], bh[s], acc1);
     __builtin_amdgcn_sched_barrier(0);
-    bh = nh;
-    bl = nl;
   }
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
@@ -984,14 +996,14 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
   S.rr = (first_skip >= 0) ? first_skip : (last >= 0 ? (last + 1) % P : S.rr);
   // deal the E-steps to the waves (LPT: heaviest first onto the least loaded wave).  Distance
   // wave w starts with the cost of its slot tiles' MFMAs (and takes at most NLS_D / NSS_D
-  // steps), E/M wave NDW + q with the M-steps of slot tiles q and q + NDW
+  // steps), E/M wave NDW + q with the M-steps of slot tiles mstep_tile(q) and + NDW
   int wcost[NW];
   for (int w = 0; w < NW; ++w) {
     wcost[w] = 0;
     if (w < NDW)
       for (int j = w; j < CW / 32; j += NDW) wcost[w] += (32 * j < nc) ? KM_COST_DIST : 0;
     else
-      for (int j = w - NDW; j < CW / 32; j += NEW)
+      for (int j = mstep_tile(w - NDW); j < CW / 32; j += NEW)
         for (int c = 32 * j; c < min(nc, 32 * j + 32); ++c)
           if (S.scl[c] >= 0) {
             wcost[w] += KM_COST_MSTEP;
@@ -1240,7 +1252,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         }
         estep_flush(S, tid, es);
       } else {
-        const int q = wave - NDW;
+        const int q = mstep_tile(wave - NDW);
         EState<NLS, NSS> es;
 #pragma unroll
         for (int i = 0; i < NLS; ++i) es.iaccL[i] = 0.f;
