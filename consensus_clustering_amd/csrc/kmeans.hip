@@ -765,10 +765,30 @@ __device__ __forceinline__ void dist_tiles(const KArgs& a, const State& S, const
                                            const h8 (&ah1)[DP / 16], const h8 (&al1)[DP / 16]) {
   using LY = Lay<DP>;
   __builtin_amdgcn_s_setprio(1);  // MFMA-dense block first in the SIMD arbiter
-  v16f acc0 = {}, acc1 = {};
   int lno = lane;
   asm volatile("" : "+v"(lno));  // per-lane offsets recomputed here (cheap), never held or spilled
   const int lro = lno & 31, hh = lno >> 5;
+  // The accumulators start at -|c|^2 / dscale (exact: dscale is a power of two), so that
+  // D = -dscale * acc = |c|^2 - dscale x.c needs no LDS read after the MFMAs (reads of |c|^2
+  // between the distance-tile stores were serialised into one LDS round trip per 8 bytes by
+  // the register-starved scheduler).
+  v16f acc0, acc1 = {};
+  {
+    const float ninv = -1.0f / a.dscale;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const float* cn = S.cnorm + 32 * (w + NDW * j) + 4 * hh;
+      v16f& acc = j ? acc1 : acc0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // slots 8g + 4hh .. +3 of the tile
+        const float4 c4 = *reinterpret_cast<const float4*>(cn + 8 * g);
+        acc[4 * g] = c4.x * ninv;
+        acc[4 * g + 1] = c4.y * ninv;
+        acc[4 * g + 2] = c4.z * ninv;
+        acc[4 * g + 3] = c4.w * ninv;
+      }
+    }
+  }
   // B operands PD k-steps ahead of the MFMAs.  Two slot tiles: one step (6 MFMAs cover the
   // read; 16 VGPRs in flight).  One slot tile (narrow sweeps, where this wave's chain sets the
   // tile time): three MFMAs per step do not cover an LDS read under DMA traffic, so three steps
@@ -799,17 +819,14 @@ __device__ __forceinline__ void dist_tiles(const KArgs& a, const State& S, const
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
     const v16f& acc = j ? acc1 : acc0;
-    const int ct = w + NDW * j;
-    float* drow = dtile + lro * DSD + 32 * ct + 4 * hh;
-    const float* cn = S.cnorm + 32 * ct + 4 * hh;
+    float* drow = dtile + lro * DSD + 32 * (w + NDW * j) + 4 * hh;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {  // slots 8g + 4hh .. +3 of the tile: one b128 store
-      const float4 c4 = *reinterpret_cast<const float4*>(cn + 8 * g);
       float4 d;
-      d.x = c4.x - a.dscale * acc[4 * g];
-      d.y = c4.y - a.dscale * acc[4 * g + 1];
-      d.z = c4.z - a.dscale * acc[4 * g + 2];
-      d.w = c4.w - a.dscale * acc[4 * g + 3];
+      d.x = -a.dscale * acc[4 * g];
+      d.y = -a.dscale * acc[4 * g + 1];
+      d.z = -a.dscale * acc[4 * g + 2];
+      d.w = -a.dscale * acc[4 * g + 3];
       *reinterpret_cast<float4*>(drow + 8 * g) = d;
     }
   }
