@@ -643,6 +643,10 @@ __device__ __forceinline__ void amin_half(const float* drow, int base, int j0, i
     col[u] = (j0 + u < cnt) ? base + 4 * (j0 + u) : CW;
     v[u] = *reinterpret_cast<const float4*>(drow + col[u]);
   }
+  // all NCH reads in flight before the first wait (the scheduler otherwise reuses one register
+  // quad for the chunks and serialises their LDS round trips)
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) asm volatile("" : "+v"(v[u].x), "+v"(v[u].y), "+v"(v[u].z), "+v"(v[u].w));
   amin_chunks<NCH>(v, col, best, lab);
 }
 
