@@ -86,7 +86,7 @@ constexpr int US = CC_KM_USTRIDE;
 // step-dealing cost units (a Lloyd step of K = 20 costs 72, a seeding step 20): the distance
 // MFMAs and the M-step of a wave's own slots, measured in the same units from the phase stamps
 #ifndef KM_COST_DIST
-#define KM_COST_DIST 80
+#define KM_COST_DIST 80  // at d = 128; the MFMA count scales with d (dist_cost)
 #endif
 #ifndef KM_COST_MSTEP
 #define KM_COST_MSTEP 65
@@ -100,6 +100,12 @@ constexpr int US = CC_KM_USTRIDE;
 #ifndef KM_COST_SSTEP
 #define KM_COST_SSTEP 20
 #endif
+#ifndef KM_COST_DIST_NARROW
+#define KM_COST_DIST_NARROW KM_COST_DIST * DP / 128
+#endif
+// The distance waves' starting cost per active slot tile for feature padding DP.
+template <int DP>
+__host__ __device__ constexpr int dist_cost() { return KM_COST_DIST_NARROW; }
 
 // Diagnostic build only (-DCC_KM_STAMPS): per-wave cycle accounting of the sweep phases of
 // workgroup 0, added into stats[8 + 8 * wave + k] (k: issue, dist, estep, mstep, commit,
@@ -933,7 +939,7 @@ __device__ __forceinline__ void msum_out(const KArgs& a, State& S, float* Sm, co
 // Thread 0: admit waiting problems into free seeding slots, then pack the next sweep:
 // seeding candidates first (they are on every problem's critical path), then Lloyd
 // problems round-robin from S.rr, first fit into the CW slots.
-__device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
+__device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_cost) {
   const int P = S.P;
   for (int p = 0; p < P && S.seedfree; ++p) {
     if (S.st[p] != ST_WAIT) continue;
@@ -1022,7 +1028,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx) {
   for (int w = 0; w < NW; ++w) {
     wcost[w] = 0;
     if (w < NDW)
-      for (int j = w; j < CW / 32; j += NDW) wcost[w] += (32 * j < nc) ? KM_COST_DIST : 0;
+      for (int j = w; j < CW / 32; j += NDW) wcost[w] += (32 * j < nc) ? dist_cost : 0;
     else
       for (int j = mstep_tile(w - NDW); j < CW / 32; j += NEW)
         for (int c = 32 * j; c < min(nc, 32 * j + 32); ++c)
@@ -1166,7 +1172,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     // ---- sweeps -----------------------------------------------------------------
     for (;;) {
       KM_STAMP(swp);
-      if (tid == 0) schedule(a, S, idx);
+      if (tid == 0) schedule(a, S, idx, dist_cost<DP>());
       __syncthreads();
       const int nitems = S.nitems, ncols = S.ncols;
       if (nitems == 0) break;
