@@ -129,7 +129,7 @@ struct KArgs {
   const uint16_t* Xhl;     // [n][2][DP] f16 bits: hi, lo of X * 2^s
   const float* xnorm;      // [n]
   int dreal;
-  float scale, inv_scale, dscale;  // 2^s, 2^-s, 2^(1-2s)
+  float scale, inv_scale, dscale, ndinv;  // 2^s, 2^-s, 2^(1-2s), -2^(2s-1) (a kernel argument: scalar)
   const int32_t* idx;
   int m, h_begin, nh, T;
   const int32_t* units;
@@ -784,7 +784,9 @@ __device__ __forceinline__ void dist_tiles(const KArgs& a, const State& S, const
   // the register-starved scheduler).
   v16f acc0, acc1 = {};
   {
-    const float ninv = -1.0f / a.dscale;
+    // d = 128: the scalar kernel argument (a VGPR copy of -1/dscale was spilled and reloaded
+    // with a vmcnt(0) before the first MFMA); d = 32 / 64 keep the per-lane value (fewer spills)
+    const float ninv = DP == 128 ? a.ndinv : -1.0f / a.dscale;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
       const float* cn = S.cnorm + 32 * (w + NDW * j) + 4 * hh;
@@ -1822,6 +1824,7 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
   a.scale = std::ldexp(1.0f, scale_exp);
   a.inv_scale = std::ldexp(1.0f, -scale_exp);
   a.dscale = std::ldexp(1.0f, 1 - 2 * scale_exp);
+  a.ndinv = -std::ldexp(1.0f, 2 * scale_exp - 1);
   a.idx = idx_hm;
   a.m = m;
   a.h_begin = h_begin;
