@@ -281,13 +281,13 @@ struct ExactK {
 
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
-// Raw dwords of step s of one row.  Bytes at or past the row's ldl (a multiple of 16) read as
-// 0xFF, and no load goes past the row.
+// Raw dwords of step s of one row, as loaded: nothing touches them until realign, so the load
+// stays in flight for a whole super-step.  No load goes past the row (the 16-B form re-reads
+// the row's last 16 bytes for a chunk at or past ldl, a multiple of 16; realign fills those
+// with 0xFF and applies the invalid-row mask).
 template <int K>
-__device__ __forceinline__ void load_raw(const uint8_t* rowp, int s, int ldl, bool valid,
-                                         uint32_t (&raw)[ExactK<K>::RAW]) {
+__device__ __forceinline__ void load_raw(const uint8_t* rowp, int s, int ldl, uint32_t (&raw)[ExactK<K>::RAW]) {
   using E = ExactK<K>;
-  const uint32_t msk = valid ? 0u : 0xFFFFFFFFu;
   if constexpr (E::DW) {
     const int a4 = (s * E::HS) & ~3;
 #pragma unroll
@@ -301,22 +301,21 @@ __device__ __forceinline__ void load_raw(const uint8_t* rowp, int s, int ldl, bo
         for (int q = 0; q < 4; ++q)
           v[q] = (o + 4 * q + 4 <= ldl) ? *reinterpret_cast<const uint32_t*>(rowp + o + 4 * q) : 0xFFFFFFFFu;
       }
-      raw[4 * c + 0] = v.x | msk;
-      raw[4 * c + 1] = v.y | msk;
-      raw[4 * c + 2] = v.z | msk;
-      raw[4 * c + 3] = v.w | msk;
+      raw[4 * c + 0] = v.x;
+      raw[4 * c + 1] = v.y;
+      raw[4 * c + 2] = v.z;
+      raw[4 * c + 3] = v.w;
     }
   } else {
     const int a16 = (s * E::HS) & ~15;
 #pragma unroll
     for (int c = 0; c < E::NC16; ++c) {  // branch-free: clamped re-reads, masked
       const int o = a16 + 16 * c;
-      const uint32_t m = (o < ldl) ? msk : 0xFFFFFFFFu;
       const uint4 v = *reinterpret_cast<const uint4*>(rowp + (o < ldl ? o : ldl - 16));
-      raw[4 * c + 0] = v.x | m;
-      raw[4 * c + 1] = v.y | m;
-      raw[4 * c + 2] = v.z | m;
-      raw[4 * c + 3] = v.w | m;
+      raw[4 * c + 0] = v.x;
+      raw[4 * c + 1] = v.y;
+      raw[4 * c + 2] = v.z;
+      raw[4 * c + 3] = v.w;
     }
   }
 }
@@ -325,9 +324,23 @@ __device__ __forceinline__ void load_raw(const uint8_t* rowp, int s, int ldl, bo
 // (the last step's tail) read as 0xFF = not sampled.  The dword shift (16-B form) is a select on
 // the wave-uniform offset (a switch made the compiler spill), the byte shift v_alignbyte.
 template <int K>
-__device__ __forceinline__ void realign(const uint32_t (&raw)[ExactK<K>::RAW], int s, int Hpad,
-                                        uint32_t (&w)[32]) {
+__device__ __forceinline__ void realign(const uint32_t (&raw_in)[ExactK<K>::RAW], int s, int Hpad, int ldl,
+                                        bool valid, uint32_t (&w)[32]) {
   using E = ExactK<K>;
+  // every raw dword counts as read here: a loaded dword that realign does not need would
+  // otherwise be reused as a temporary, and that write-after-load stalls on the label load
+  // (issued one step ago) at the top of the next super-step instead of here
+#pragma unroll
+  for (int j = 0; j < E::RAW; ++j) asm volatile("" ::"v"(raw_in[j]));
+  uint32_t raw[E::RAW];
+#pragma unroll
+  for (int j = 0; j < E::RAW; ++j) raw[j] = raw_in[j];
+  if constexpr (!E::DW) {  // chunks at or past ldl (clamped re-reads) read as 0xFF
+    const int a16 = (s * E::HS) & ~15;
+#pragma unroll
+    for (int j = 0; j < E::RAW; ++j)
+      if (a16 + 16 * (j / 4) >= ldl) raw[j] = 0xFFFFFFFFu;  // wave-uniform
+  }
   const int off = (s * E::HS) & (E::DW ? 3 : 15);  // wave-uniform
   const int bsh = off & 3;
   if constexpr (E::DW) {
@@ -345,6 +358,10 @@ __device__ __forceinline__ void realign(const uint32_t (&raw)[ExactK<K>::RAW], i
     }
 #pragma unroll
     for (int i = 0; i < E::NWX; ++i) w[i] = __builtin_amdgcn_alignbyte(sh[i + 1], sh[i], bsh);
+  }
+  if (!valid) {  // a row past n: not sampled in any resample
+#pragma unroll
+    for (int i = 0; i < E::NWX; ++i) w[i] = 0xFFFFFFFFu;
   }
   const int rem = Hpad - s * E::HS;
   if (rem < E::HS) {  // wave-uniform: the last step
@@ -437,8 +454,8 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
   constexpr int NRW = EX ? ExactK<EX ? KP : 3>::RAW : 1;
   uint32_t raw1[NRW];  // exact K: raw chunks of step s+2 (one step in flight; two measured slower)
   if constexpr (EX) {
-    load_raw<KP>(rowp, 0, ldl, evalid, raw1);
-    realign<KP>(raw1, 0, Hpad, w);
+    load_raw<KP>(rowp, 0, ldl, raw1);
+    realign<KP>(raw1, 0, Hpad, ldl, evalid, w);
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       uint32_t oc[8];
@@ -446,9 +463,9 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
 #pragma unroll
       for (int q = 0; q < 8; ++q) o[8 * kc + q] = oc[q];
     }
-    load_raw<KP>(rowp, nsteps > 1 ? 1 : 0, ldl, evalid, raw1);
-    realign<KP>(raw1, nsteps > 1 ? 1 : 0, Hpad, w);  // step 1
-    load_raw<KP>(rowp, nsteps > 2 ? 2 : 0, ldl, evalid, raw1);  // step 2
+    load_raw<KP>(rowp, nsteps > 1 ? 1 : 0, ldl, raw1);
+    realign<KP>(raw1, nsteps > 1 ? 1 : 0, Hpad, ldl, evalid, w);  // step 1
+    load_raw<KP>(rowp, nsteps > 2 ? 2 : 0, ldl, raw1);  // step 2
   } else {
     load_labels<KP>(rowp, evalid, w);
     expand<KP>(w, o);
@@ -526,8 +543,8 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     }
     if constexpr (EX) {
       // w <- step s+2 (loaded one step ago), raw1 <- step s+3
-      realign<KP>(raw1, (s + 2) < nsteps ? s + 2 : s, Hpad, w);
-      load_raw<KP>(rowp, (s + 3) < nsteps ? s + 3 : s, ldl, evalid, raw1);
+      realign<KP>(raw1, (s + 2) < nsteps ? s + 2 : s, Hpad, ldl, evalid, w);
+      load_raw<KP>(rowp, (s + 3) < nsteps ? s + 3 : s, ldl, raw1);
     } else if constexpr (PF2) {
       // rotate the label prefetch: w <- step s+2, wn <- step s+3 (clamped re-reads at the end)
 #pragma unroll
