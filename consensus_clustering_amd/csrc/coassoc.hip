@@ -640,10 +640,35 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
         for (int nj = 0; nj < 2; ++nj) {
           const uint4 q0 = it4[(mi * 2 + nj) * 2], q1 = it4[(mi * 2 + nj) * 2 + 1];
           const uint32_t iw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+          // table_bin_r for the block's 16 elements in three batched LDS passes (reciprocals,
+          // then both thresholds, then the counter adds): one element at a time, every
+          // element was two dependent LDS round trips, each behind the previous add
+          uint32_t ival[16];
+          float rc[16];
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
-            const uint32_t ival = (iw[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
-            const int b = table_bin_r(static_cast<uint32_t>(acc[mi][nj][v]), ival, tab, rtab);
+            ival[v] = (iw[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
+            rc[v] = rtab[ival[v]];
+          }
+#pragma unroll
+          for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(rc[v]));
+          int g[16];
+          uint32_t lo[16], hi[16];
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const uint32_t m = static_cast<uint32_t>(acc[mi][nj][v]);
+            g[v] = static_cast<int>(static_cast<float>(m) * rc[v]);
+            g[v] = g[v] > NBINS - 1 ? NBINS - 1 : g[v];
+            const uint16_t* row = tab + ival[v] * BT_ROW;
+            lo[v] = row[g[v]];
+            hi[v] = row[g[v] + 1];
+          }
+#pragma unroll
+          for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(lo[v]), "+v"(hi[v]));
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const uint32_t m = static_cast<uint32_t>(acc[mi][nj][v]);
+            const int b = g[v] - (m < lo[v] ? 1 : 0) + (m >= hi[v] ? 1 : 0);
             atomicAdd(&hist[b * NT + tid], 1u);
           }
         }
