@@ -495,12 +495,25 @@ __device__ void kpp_select(const KArgs& a, St& S, int p, const float* closest, i
     if (j < T) {
       const float* rowp = closest + RT * j;
       const int nr = min(RT, m - RT * j);
-      for (int r = 0; r < nr; r += 4) {
-        const float4 q = *reinterpret_cast<const float4*>(rowp + r);  // m, RT multiples of 4 or tail
-        v += static_cast<double>(q.x);
-        if (r + 1 < nr) v += static_cast<double>(q.y);
-        if (r + 2 < nr) v += static_cast<double>(q.z);
-        if (r + 3 < nr) v += static_cast<double>(q.w);
+      if (nr == RT) {  // a full tile: all its loads in flight, then the same in-order f64 sum
+        float4 q[RT / 4];
+#pragma unroll
+        for (int r4 = 0; r4 < RT / 4; ++r4) q[r4] = *reinterpret_cast<const float4*>(rowp + 4 * r4);
+#pragma unroll
+        for (int r4 = 0; r4 < RT / 4; ++r4) {
+          v += static_cast<double>(q[r4].x);
+          v += static_cast<double>(q[r4].y);
+          v += static_cast<double>(q[r4].z);
+          v += static_cast<double>(q[r4].w);
+        }
+      } else {
+        for (int r = 0; r < nr; r += 4) {
+          const float4 q = *reinterpret_cast<const float4*>(rowp + r);  // m, RT multiples of 4 or tail
+          v += static_cast<double>(q.x);
+          if (r + 1 < nr) v += static_cast<double>(q.y);
+          if (r + 2 < nr) v += static_cast<double>(q.z);
+          if (r + 3 < nr) v += static_cast<double>(q.w);
+        }
       }
     }
 #pragma unroll
@@ -1426,25 +1439,27 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       }
 
       // ---- labels changed? (RUN items): compare this sweep's label buffer with the previous
-      // one, 16 B per thread and load; then this sweep's buffer becomes the current one
+      // one, 16 B per thread and load, every item in one pass (flags set by any thread that sees
+      // a difference: one barrier for all items instead of one per item); then this sweep's
+      // buffer becomes the current one
+      if (tid < nitems) S.ichanged[tid] = 0;
+      __syncthreads();
       for (int it = 0; it < nitems; ++it) {
-        if (S.ikind[it] < IK_RUN) continue;
+        if (S.ikind[it] != IK_RUN) continue;
         const int p = S.iprob[it];
+        const uint4* cur = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + 1 - S.lcur[p]) * a.lsm);
+        const uint4* old = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm);
         bool diff = false;
-        if (S.ikind[it] == IK_RUN) {
-          const uint4* cur = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + 1 - S.lcur[p]) * a.lsm);
-          const uint4* old = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm);
-          for (int e = tid; e < (m + 15) / 16; e += NT) {
-            const uint4 x = cur[e], y = old[e];
-            diff |= (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
-          }
+        for (int e = tid; e < (m + 15) / 16; e += NT) {
+          const uint4 x = cur[e], y = old[e];
+          diff |= (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
         }
-        const int any = __syncthreads_or(diff);
-        if (tid == 0) {
-          S.ichanged[it] = any != 0;
-          S.lcur[p] = static_cast<unsigned char>(1 - S.lcur[p]);
-        }
+        if (diff) S.ichanged[it] = 1;
       }
+      __syncthreads();
+      if (tid == 0)
+        for (int it = 0; it < nitems; ++it)
+          if (S.ikind[it] >= IK_RUN) S.lcur[S.iprob[it]] = static_cast<unsigned char>(1 - S.lcur[S.iprob[it]]);
       __syncthreads();
 
       // ---- Lloyd M-step completion (RUN items) ------------------------------------
