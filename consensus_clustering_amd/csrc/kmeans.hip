@@ -89,10 +89,10 @@ constexpr int US = CC_KM_USTRIDE;
 #define KM_COST_DIST 80  // at d = 128; the MFMA count scales with d (dist_cost)
 #endif
 #ifndef KM_COST_MSTEP
-#define KM_COST_MSTEP 65
+#define KM_COST_MSTEP 50
 #endif
 #ifndef KM_COST_LBASE
-#define KM_COST_LBASE 24
+#define KM_COST_LBASE 32
 #endif
 #ifndef KM_COST_LCHUNK
 #define KM_COST_LCHUNK 16
