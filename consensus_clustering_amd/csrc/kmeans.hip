@@ -83,7 +83,7 @@ constexpr int KMAX = 127;
 constexpr int DSD = CW + 4;         // distance-tile row stride (floats): 16-B rows, conflict-free b128
 constexpr int NRING = 4;            // X tile ring: t+1 (gather), t (dist), t-2 (M-step)
 constexpr int US = CC_KM_USTRIDE;
-// step-dealing cost units (a Lloyd step of K = 20 costs 72, a seeding step 20): the distance
+// step-dealing cost units (a Lloyd step of K = 20 costs 80, a seeding step 20): the distance
 // MFMAs and the M-step of a wave's own slots, measured in the same units from the phase stamps
 #ifndef KM_COST_DIST
 #define KM_COST_DIST 80  // at d = 128; the MFMA count scales with d (dist_cost)
