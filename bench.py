@@ -11,11 +11,15 @@ strong scaling: the ranks split the fixed fit (resamples for k-means, triangle t
 for co-association).  Rank 0 prints ONE JSON line.
 
 ``roofline`` is the dominant kernel (cc_kmeans_batched, MFMA-bound): ALGORITHMIC flops
-(2·d per row×centroid distance product of Lloyd and k-means++, + d per M-step row update;
-the kernel counts them) ÷ the launches' HIP-event durations on the launch stream, against
-the f32-class ceiling of the f16 hi/lo MFMA scheme (2516.6 TF f16 dense / 3 = 838.9 TF).  ``cpu_baseline`` times the oracle (numpy +
-scikit-learn, the reference's algorithm) on a bounded sample of the same workload on
-this host and extrapolates to resample-clusterings/s (rank 0, N=1 only).
+FLOP_KM of SURVEY.md §8d (2·d per row×centroid distance product of Lloyd and k-means++; the
+kernel counts the products) ÷ the launches' HIP-event durations on the launch stream, against
+the f32-class ceiling of the f16 hi/lo MFMA scheme (2516.6 TF f16 dense / 3 = 838.9 TF).  The
+M-step's d flops per (row, running problem) update are not part of §8d's FLOP_KM; they are
+reported beside it (``mstep_flops_per_launch``, ``frac_incl_mstep``).  A fraction above 1
+means the timed launches did not do the credited work: the bench refuses to report it.
+``cpu_baseline`` times the oracle (numpy + scikit-learn, the reference's algorithm) on a
+bounded sample of the same workload on this host's usable cores and extrapolates to
+resample-clusterings/s (rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -125,7 +129,7 @@ def cpu_baseline(cfg, X, H_sample=8):
 
     n, H, frac = cfg["n"], cfg["H"], cfg["frac"]
     Ks = cfg["Ks"]
-    cores = min(16, os.cpu_count() or 1)
+    cores = usable_cores()
     Hs = min(H, H_sample)
     idx = O.subsampling_indices(n, Hs, frac, SEED)
     t0 = time.perf_counter()
@@ -170,6 +174,46 @@ def cpu_baseline(cfg, X, H_sample=8):
     }
 
 
+def usable_cores() -> int:
+    """CPUs this process may run on (its affinity mask), not the machine's total."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        return os.cpu_count() or 1
+
+
+def band_pairs(n: int, tile_begin: int, tile_end: int, T: int = 256) -> int:
+    """Strict-upper pairs (i < j < n) inside the upper-triangle tiles [tile_begin, tile_end),
+    numbered row-major as cc_coassoc numbers them (tile (bi, bj), bi <= bj)."""
+    nb = (n + T - 1) // T
+    total, t = 0, 0
+    for bi in range(nb):
+        row_tiles = nb - bi
+        lo, hi = max(tile_begin, t), min(tile_end, t + row_tiles)
+        if lo < hi:
+            rows = min(n, (bi + 1) * T) - bi * T
+            for bj in range(bi + (lo - t), bi + (hi - t)):
+                if bj == bi:
+                    total += rows * (rows - 1) // 2
+                else:
+                    total += rows * (min(n, (bj + 1) * T) - bj * T)
+        t += row_tiles
+    return total
+
+
+def checked_frac(achieved, peak, what):
+    """achieved / peak, or None (with a note on stderr) when it exceeds 1: a fraction above the
+    roof means the timed launches did not do the credited work."""
+    if peak <= 0:
+        return None
+    f = achieved / peak
+    if f > 1.0:
+        print(f"[bench] REFUSED: {what} roofline fraction {f:.3f} > 1 (credited work was not all "
+              "done by the timed launches)", file=sys.stderr, flush=True)
+        return None
+    return f
+
+
 def load_traffic(config, kernel, key="bytes_per_launch", prefix="profiles"):
     """HBM bytes of `kernel` at `config` (per launch, or per fit with key="bytes_per_fit") from a
     committed PMC summary (profiles/traffic/<config>_<kernel>.json, tools/traffic_summary.py), or
@@ -206,6 +250,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from consensus_clustering_amd import ConsensusClustering, engine
+    from consensus_clustering_amd.dist import shard as dist_shard
 
     if cfg.get("data") == "expression":
         X = make_expression_f32(cfg["n"], cfg["d"], groups=cfg["k_true"], seed=SEED)
@@ -258,20 +303,39 @@ def main():
         tdist.all_reduce(ktime, op=tdist.ReduceOp.SUM)
     elapsed = float(vec[0])
     d = cfg["d"]
-    flops = 2.0 * d * (float(st[0]) + float(st[1])) + d * float(st[2])
+    # FLOP_KM: 2 d per distance product of Lloyd sweeps and k-means++ candidate
+    # passes, counted by the kernel (st[0], st[1]); the M-step's d per (row, running problem)
+    # update (st[2]) is reported separately
+    flops = 2.0 * d * (float(st[0]) + float(st[1]))
+    mstep_flops = d * float(st[2])
     km_ms_tot, km_launches = float(ktime[0]), max(float(ktime[1]), 1.0)
     achieved = flops / (km_ms_tot * 1e-3) / 1e12 if km_ms_tot > 0 else 0.0
+    achieved_m = (flops + mstep_flops) / (km_ms_tot * 1e-3) / 1e12 if km_ms_tot > 0 else 0.0
     clusterings = cfg["H"] * len(cfg["Ks"]) * args.steps
     value = clusterings / elapsed
     # co-association: OPS_M = sum_K 2 P H K per fit (channel padding and the
-    # diagonal tiles' lower halves not credited) over the HIP-event time of its launches
-    P = cfg["n"] * (cfg["n"] - 1) / 2
-    co_ops = sum(2.0 * P * cfg["H"] * K for K in cfg["Ks"]) * args.steps
+    # diagonal tiles' lower halves not credited) over the HIP-event time of its launches.  A
+    # rehearsal (or a rank of an N-GPU run) is credited only the pairs of its own tile band.
+    n_ = cfg["n"]
+    if args.rehearse or world > 1:
+        r_, w_ = ((int(v) for v in args.rehearse.split("/")) if args.rehearse else (rank, world))
+        nt_ = (((n_ + 255) // 256) * ((n_ + 255) // 256 + 1)) // 2
+        tb_, te_ = dist_shard(nt_, r_, w_)  # the fit's own tile split (api.py, dist.shard)
+        P = float(band_pairs(n_, tb_, te_))
+    else:
+        P = n_ * (n_ - 1) / 2
+    co_ops_t = torch.tensor([sum(2.0 * P * cfg["H"] * K for K in cfg["Ks"]) * args.steps],
+                            dtype=torch.float64, device=dev)
+    if world > 1:
+        tdist.all_reduce(co_ops_t, op=tdist.ReduceOp.SUM)
+    co_ops = float(co_ops_t[0])
     co_ms_tot = float(ktime[2])
     co_achieved = co_ops / (co_ms_tot * 1e-3) / 1e12 if co_ms_tot > 0 else 0.0
+    # per-config traffic files hold full single-GPU fits: not valid for a partial (rehearsal) run
+    full_fit = not args.rehearse
 
     if rank == 0:
-        traffic = load_traffic(args.config, km_kernel)
+        traffic = load_traffic(args.config, km_kernel) if full_fit and world == 1 else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -296,12 +360,15 @@ def main():
                 "achieved": achieved,
                 "peak": KMEANS_PEAK_TF,
                 "unit": "TFLOP/s",
-                "frac": achieved / KMEANS_PEAK_TF,
+                "frac": checked_frac(achieved, KMEANS_PEAK_TF, "k-means"),
                 "peak_note": "f16 dense MFMA peak 2516.6 TF / 3 (f32-class product = 3 f16 MFMAs)",
+                "flops_note": "FLOP_KM of SURVEY.md §8d: 2*d per Lloyd and k-means++ distance product",
                 "sweeps": float(st[4]), "slot_tile_row_tiles": float(st[5]),
                 "relocations": float(st[3]),
                 "traffic": traffic,
                 "flops_per_launch": flops / km_launches,
+                "mstep_flops_per_launch": mstep_flops / km_launches,
+                "frac_incl_mstep": checked_frac(achieved_m, KMEANS_PEAK_TF, "k-means incl. M-step"),
                 "avg_launch_ms": km_ms_tot / km_launches,
             },
             "roofline_coassoc": {
@@ -310,10 +377,11 @@ def main():
                 "achieved": co_achieved,
                 "peak": I8_MFMA_PEAK_TOPS,
                 "unit": "TOP/s",
-                "frac": co_achieved / I8_MFMA_PEAK_TOPS,
+                "frac": checked_frac(co_achieved, I8_MFMA_PEAK_TOPS, "co-association"),
                 "ops_per_fit": co_ops / args.steps,
                 "ms_per_fit": co_ms_tot / args.steps,
-                "traffic": load_traffic(args.config, "cc_coassoc", key="bytes_per_fit"),
+                "traffic": (load_traffic(args.config, "cc_coassoc", key="bytes_per_fit")
+                            if full_fit and world == 1 else None),
                 "note": "the 20-bin histogram (K5) is fused into this kernel's epilogue: no HBM pass",
             },
             "kernels_ms_per_step": {k: v[1] / args.steps for k, v in timers.items()},

@@ -29,6 +29,7 @@ SIGNATURES = {
     "cc_random_sample": (_c_int, [_c_u32, _c_i64, _vp]),
     "cc_num_tiles": (_c_i64, [_c_int]),
     "cc_scatter_labels": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
+    "cc_copy_label_columns": (_c_int, [_vp, _c_i64, _c_int, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp]),
     "cc_cosample": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp]),
     "cc_coassoc": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp,
                             _vp, _vp, _c_int, _vp]),

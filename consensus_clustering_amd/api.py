@@ -16,7 +16,7 @@ What runs where (``fit``):
   I, M, histogram int8-MFMA tiles of the upper triangle (cc_cosample / cc_coassoc)
   hist/cdf/PAC    host float64 from 20 exact integer counts (post.py)
   multi-GPU       resamples and triangle tiles sharded over torch.distributed ranks
-                  (dist.py); RCCL MIN-merge of labels, SUM of counts
+                  (dist.py); RCCL all-gather of each rank's label columns, SUM of counts
 
 Deliberate differences, all documented in DESIGN.md: the constructor does not delete
 files in ``memmap_folder`` (CC.py:83-86); the n x n matrices are materialised only when
@@ -158,6 +158,13 @@ class ConsensusClustering:
         m = int(self.subsampling * n)
         Ks = [int(K) for K in self.K_range]
         self._check_k_range(Ks)
+        # the reference seeds resample h with random_state + h (CC.py:232): validate the whole
+        # H range once, on every rank, before sharding (a rank-local check would let the other
+        # ranks go on into the exchanges and hang)
+        if self.random_state is None:
+            raise TypeError("unsupported operand type(s) for +: 'NoneType' and 'int'")
+        if H > 0 and (int(self.random_state) < 0 or int(self.random_state) + H - 1 > 2**32 - 1):
+            raise ValueError("Seed must be between 0 and 2**32 - 1")
         rank, W = dist.world()
         self.partial_ = False
         if self._rehearsal is not None:
@@ -247,7 +254,7 @@ class ConsensusClustering:
                     raise ValueError(f"clusterer labels must lie in [0, {K})")
                 engine.scatter_labels(idx_d[h0:h1].contiguous(), torch.from_numpy(lab).to(dev), n,
                                       labels[k], h_offset=h0)
-        dist.merge_labels(labels)
+        dist.merge_labels(labels, H)
         torch.cuda.synchronize(dev)
         t_cl = time.perf_counter()
 
@@ -411,13 +418,16 @@ class ConsensusClustering:
     def _plot_cdf(self, ax=None):
         """Consensus CDF per K as a step curve over the bin upper edges, with the PAC interval
         shaded (the ``plot_cdf`` option of CC.py:133-134; presentation only, host matplotlib).
-        Returns the axes, or None when matplotlib is not installed."""
+        With no ``ax`` it opens a new figure and shows it, as the reference does; pass ``ax`` to
+        draw into an existing figure.  Returns the axes, or None when matplotlib is not
+        installed."""
         try:
             import matplotlib.pyplot as plt
         except ImportError:  # pragma: no cover
             return None
-        if ax is None:
-            ax = plt.gca()
+        show = ax is None
+        if show:
+            ax = plt.figure().gca()
         lo, hi = self.PAC_interval
         ax.axvspan(lo, hi, color='0.9', zorder=0)
         for K, res in self.cdf_at_K_data.items():
@@ -428,6 +438,8 @@ class ConsensusClustering:
         ax.set_xlabel('consensus value')
         ax.set_ylabel('fraction of pairs <= value')
         ax.legend(fontsize='small')
+        if show:
+            plt.show()
         return ax
 
 

@@ -734,6 +734,22 @@ __global__ void scatter_labels_kernel(const int32_t* __restrict__ idx, const int
   }
 }
 
+// dst[r * ld_dst + col_dst + j] = src[r * ld_src + col_src + j] for r < rows, j < width: a
+// window of resample columns between two sample-major label matrices (the multi-GPU label
+// exchange packs a rank's own columns before the all-gather and places every rank's columns
+// after it).  One thread per byte of the window; consecutive threads read consecutive bytes.
+__global__ void copy_label_columns_kernel(const uint8_t* __restrict__ src, int64_t ld_src, int col_src,
+                                          uint8_t* __restrict__ dst, int64_t ld_dst, int col_dst,
+                                          int64_t rows, int width) {
+  const int64_t total = rows * width;
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t r = e / width;
+    const int j = static_cast<int>(e - r * width);
+    dst[r * ld_dst + col_dst + j] = src[r * ld_src + col_src + j];
+  }
+}
+
 __global__ void consensus_kernel(const int32_t* __restrict__ M, const int32_t* __restrict__ I,
                                  int n, float* __restrict__ C) {
   const int64_t total = static_cast<int64_t>(n) * n;
@@ -802,6 +818,21 @@ extern "C" int cc_scatter_labels(const int32_t* idx_hm, const int32_t* labels_hm
                      static_cast<hipStream_t>(stream), idx_hm, labels_hm, H, m, n,
                      reinterpret_cast<uint8_t*>(labels_nh), ldl);
   return launch_status("cc_scatter_labels");
+}
+
+extern "C" int cc_copy_label_columns(const uint8_t* src, int64_t ld_src, int col_src, uint8_t* dst,
+                                     int64_t ld_dst, int col_dst, int64_t rows, int width, void* stream) {
+  if (rows < 0 || width < 0 || col_src < 0 || col_dst < 0 || col_src + static_cast<int64_t>(width) > ld_src ||
+      col_dst + static_cast<int64_t>(width) > ld_dst || ((!src || !dst) && rows * width > 0)) {
+    cc::set_error("cc_copy_label_columns: bad arguments (the window must lie inside both row strides)");
+    return CC_ERR_ARG;
+  }
+  const int64_t total = rows * width;
+  if (total == 0) return CC_OK;
+  const int blocks = static_cast<int>(std::min<int64_t>((total + 255) / 256, 16384));
+  hipLaunchKernelGGL(copy_label_columns_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     src, ld_src, col_src, dst, ld_dst, col_dst, rows, width);
+  return launch_status("cc_copy_label_columns");
 }
 
 extern "C" int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, int64_t tile_begin,

@@ -266,6 +266,13 @@ extern "C" int cc_kmeans_fit(const void* X, int n, int d, const int32_t* idx_hm,
     return CC_ERR_HIP;
   }
   if (precision == CC_KM_FAST && P.dpad <= 128 && P.nU <= 0) return P.nU;
+  // reject an undersized workspace before anything is carved from it or copied into it: the
+  // tables, plus the row image on the float32 path (the engine's own share is checked below)
+  const size_t need_pre = P.tables_bytes + (precision == CC_KM_FAST ? P.rows_bytes : 0);
+  if (ws_bytes < need_pre) {
+    cc::set_error("cc_kmeans_fit: workspace too small");
+    return CC_ERR_ARG;
+  }
   const hipStream_t st = static_cast<hipStream_t>(stream);
   char* w = static_cast<char*>(workspace);
   size_t off = 0;

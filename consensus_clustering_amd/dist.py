@@ -5,9 +5,12 @@ ndarray / np.memmap (CC.py:185-195, :290).  Here every (resample, K) problem is
 independent and every count is an integer sum, so a fit shards exactly:
 
 * resamples   rank r runs k-means for h in ``shard(H, r, W)`` (no communication);
-* labels      the per-rank uint8 label matrices hold 0xFF outside their resamples, so
-              an element-wise MIN all-reduce assembles the full [nK, n, Hpad] matrix
-              (RCCL over xGMI on the GPU; gloo in the CPU tests);
+* labels      each rank packs its own resample columns [h0, h1) of the sample-major
+              [nK, n, Hpad] label matrix into a contiguous [nK, n, hw] block
+              (hw = ceil(H / W)), the blocks are ALL-GATHERED (RCCL over xGMI on the GPU;
+              gloo in the CPU tests) and every block is placed back at its columns.  Per GPU
+              that moves (W-1)/W of nK n H bytes; a MIN all-reduce of the whole matrix (the
+              round-2 exchange) moved 2 (W-1)/W of nK n Hpad;
 * triangle    rank r owns tiles ``shard(num_tiles, r, W)`` of the upper-triangle
               tiling (contiguous, equal-cost tiles: row-band sharding) and computes
               I, M and the histogram of its band only;
@@ -56,9 +59,45 @@ def _all_reduce(t: torch.Tensor, op) -> torch.Tensor:
     return t
 
 
-def merge_labels(labels: torch.Tensor) -> torch.Tensor:
-    """Assemble per-rank label matrices (0xFF where not owned) in place."""
-    return _all_reduce(labels, dist.ReduceOp.MIN)
+def _copy_columns(src, col_src, dst, col_dst, width):
+    if src.is_cuda:
+        from . import engine
+
+        engine.copy_label_columns(src, col_src, dst, col_dst, width)
+    else:  # CPU tensors occur only in the gloo CPU tests of this exchange
+        dst[..., col_dst:col_dst + width].copy_(src[..., col_src:col_src + width])
+
+
+def merge_labels(labels: torch.Tensor, H: int) -> torch.Tensor:
+    """Assemble the full label matrix in place from every rank's own resample columns.
+
+    labels: uint8 [nK, n, Hpad] (contiguous), this rank's columns ``shard(H, rank, W)`` filled
+    (0xFF = not sampled).  After the call every rank holds every rank's columns.  Only the
+    resample columns travel: a packed [nK, n, hw] block per rank, all-gathered."""
+    if not (_live() and dist.get_world_size() > 1):
+        return labels
+    rank, W = world()
+    assert labels.is_contiguous() and labels.dtype == torch.uint8
+    hw = -(-int(H) // W)
+    lead = tuple(labels.shape[:-1])
+    h0, h1 = shard(H, rank, W)
+    stage = torch.full(lead + (hw,), 0xFF, dtype=torch.uint8, device=labels.device)
+    _copy_columns(labels, h0, stage, 0, h1 - h0)
+    if labels.is_cuda and dist.get_backend() != "gloo":
+        gathered = torch.empty((W,) + lead + (hw,), dtype=torch.uint8, device=labels.device)
+        dist.all_gather_into_tensor(gathered, stage)
+        blocks = list(gathered.unbind(0))
+    else:
+        host = stage.cpu()
+        parts = [torch.empty_like(host) for _ in range(W)]
+        dist.all_gather(parts, host)
+        blocks = [p.to(labels.device) for p in parts]
+    for r, blk in enumerate(blocks):
+        if r == rank:
+            continue
+        a, b = shard(H, r, W)
+        _copy_columns(blk.contiguous(), 0, labels, a, b - a)
+    return labels
 
 
 def sum_counts(t: torch.Tensor) -> torch.Tensor:

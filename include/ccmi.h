@@ -14,6 +14,7 @@
  *   cc_resample_indices   CC.py:216-241  _get_subsampling_indices (numpy RandomState replay)
  *   cc_resample_device    the same on the device (n <= 65536), straight into HBM
  *   cc_scatter_labels     CC.py:260-262, :284-285  indicator / one-hot row placement
+ *   cc_copy_label_columns CC.py:185-195 (the parallel paths' shared M) -> multi-GPU label exchange
  *   cc_cosample           CC.py:264  I = S^T S            (int8 MFMA, upper-triangle tiles)
  *   cc_coassoc            CC.py:287-290 + :338-344  M += L^T L fused with the 20-bin histogram
  *   cc_consensus          CC.py:372-373  C = f32(M) / f32(I + 1e-6), diag 1
@@ -82,6 +83,15 @@ int cc_resample_device(uint32_t seed, int h_begin, int h_end, int n, int m, int3
  * labels_nh must be pre-filled with 0xFF (= not sampled).  (CC.py:260-262, :284-285) */
 int cc_scatter_labels(const int32_t* idx_hm, const int32_t* labels_hm, int H, int m, int n,
                       int8_t* labels_nh, int ldl, void* stream);
+
+/* dst[r*ld_dst + col_dst + j] = src[r*ld_src + col_src + j] for r < rows, j < width (bytes).
+ * Moves a window of resample columns between sample-major label matrices ([rows][ld] uint8):
+ * the multi-GPU exchange packs a rank's own columns [h0, h1) into a contiguous block before an
+ * all-gather and places each rank's block at its columns afterwards.  It replaces the
+ * reference's shared in-place M of its parallel paths (CC.py:185-195): labels, not n x n
+ * counts, cross the links.  Asynchronous on `stream`. */
+int cc_copy_label_columns(const uint8_t* src, int64_t ld_src, int col_src, uint8_t* dst,
+                          int64_t ld_dst, int col_dst, int64_t rows, int width, void* stream);
 
 /* Co-sampling counts I_ij = #{h : i and j both sampled} for the tiles
  * [tile_begin, tile_end) of the upper-triangle tiling (CC.py:264).

@@ -1,0 +1,41 @@
+"""Host-side API behaviour that needs no GPU: argument checks that run before any device work,
+and the CDF plot (CC.py:133-134, :389-410)."""
+import numpy as np
+import pytest
+
+from consensus_clustering_amd import ConsensusClustering, post
+
+
+def test_seed_range_checked_for_all_resamples_before_sharding():
+    """CC.py:232 seeds resample h with random_state + h; the whole H range is validated up front
+    (on every rank), not per shard."""
+    X = np.zeros((10, 2), dtype=np.float32)
+    with pytest.raises(TypeError):
+        ConsensusClustering(K_range=[2], n_iterations=5, random_state=None, plot_cdf=False).fit(X)
+    with pytest.raises(ValueError, match="Seed must be between"):
+        ConsensusClustering(K_range=[2], n_iterations=10, random_state=2**32 - 5,
+                            plot_cdf=False).fit(X)
+    with pytest.raises(ValueError, match="Seed must be between"):
+        ConsensusClustering(K_range=[2], n_iterations=3, random_state=-1, plot_cdf=False).fit(X)
+
+
+def test_plot_cdf_opens_and_shows_a_figure(monkeypatch):
+    mpl = pytest.importorskip("matplotlib")
+    mpl.use("Agg")
+    import matplotlib.pyplot as plt
+
+    shown = []
+    monkeypatch.setattr(plt, "show", lambda *a, **k: shown.append(True))
+    cc = ConsensusClustering(K_range=[2, 3], random_state=0, plot_cdf=True)
+    counts = np.arange(20, dtype=np.int64) + 1
+    cc.cdf_at_K_data = {}
+    for K in (2, 3):
+        hist, cdf, edges, pac = post.cdf_from_counts(counts * K)
+        cc.cdf_at_K_data[K] = dict(hist=hist, cdf=cdf, bin_edges=edges, pac_area=pac)
+    nfig = len(plt.get_fignums())
+    ax = cc._plot_cdf()
+    assert shown == [True] and len(plt.get_fignums()) == nfig + 1
+    assert len(ax.get_lines()) == 2
+    fig, ax2 = plt.subplots()
+    assert cc._plot_cdf(ax=ax2) is ax2 and shown == [True]  # embedding: no show
+    plt.close("all")

@@ -1,5 +1,5 @@
 """Multi-process (world_size 2, gloo, CPU) check of the multi-GPU plan in dist.py:
-resample sharding + MIN-merge of label matrices, row-band sharding of the triangle tiles,
+resample sharding + all-gather of each rank's label columns, row-band sharding of the triangle tiles,
 SUM of histogram counts.  The per-rank compute is the CPU oracle restricted to the rank's
 resamples / tiles, so what is tested is exactly the partition and the exchange."""
 import os
@@ -66,7 +66,7 @@ def _worker(rank, world, port, name, out):
             for h in range(h0, h1):
                 L[k, torch.from_numpy(f["indices"][h].astype(np.int64)), h] = torch.from_numpy(
                     f["labels"][k, h].astype(np.uint8))
-        cdist.merge_labels(L)
+        cdist.merge_labels(L, H)
         full = np.full((len(Ks), n, H), 0xFF, np.uint8)
         for k in range(len(Ks)):
             for h in range(H):
@@ -90,10 +90,12 @@ def _worker(rank, world, port, name, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["blobs_n400_d8_k4", "c1_corr_raw"])
-def test_two_rank_plan_is_exact(tmp_path, name):
+@pytest.mark.parametrize("name,world", [("blobs_n400_d8_k4", 2), ("c1_corr_raw", 2),
+                                        ("c1_corr_raw", 3)])
+def test_multi_rank_plan_is_exact(tmp_path, name, world):
+    """World 2 and 3 (uneven resample shards: the gathered blocks are padded to ceil(H/W))."""
     out = str(tmp_path / "counts.npy")
-    mp.spawn(_worker, args=(2, _free_port(), name, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), name, out), nprocs=world, join=True)
     counts = np.load(out)
     from consensus_clustering_amd import post
     from oracle import cc_oracle as O

@@ -84,3 +84,28 @@ def test_one_call_rejects_bad_k():
     idx_d = torch.from_numpy(engine.resample_indices(0, 100, 80, 0, 2)).to(dev)
     with pytest.raises(_lib.CCMIError):
         _fit_abi(X, [2, 128], 2, 80, 0, 2, idx_d, 0)
+
+
+@pytest.mark.parametrize("precision,dtype", [(0, np.float32), (1, np.float64)])
+def test_undersized_workspace_is_rejected(precision, dtype):
+    """cc_kmeans_fit checks the workspace before it carves or uploads anything: a workspace
+    smaller than the tables (and, on the float32 path, the row image) is CC_ERR_ARG, and the
+    guard bytes past it stay untouched."""
+    dev = engine.require_gpu()
+    n, d, Ks, H = 500, 16, [2, 3], 4
+    m = int(0.8 * n)
+    X = _blobs(n, d, 3, seed=1, dtype=dtype)
+    Xd = torch.from_numpy(X).to(dev)
+    idx_d = torch.from_numpy(engine.resample_indices(1, n, m, 0, H)).to(dev)
+    L = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
+    Ks_np = np.asarray(Ks, dtype=np.int32)
+    guard = torch.full((1 << 16,), 0x5A, dtype=torch.uint8, device=dev)
+    for small in (0, 256, 4096):
+        with pytest.raises(_lib.CCMIError, match="workspace too small"):
+            _lib.call("cc_kmeans_fit", Xd.data_ptr(), n, d, idx_d.data_ptr(), H, m, 0, H,
+                      Ks_np.ctypes.data, len(Ks), 3, 300, 1e-4, ctypes.c_uint32(1), precision,
+                      L.data_ptr(), L.stride(1), None, None, guard.data_ptr(), small,
+                      engine.stream_ptr(dev))
+    torch.cuda.synchronize()
+    assert bool((guard == 0x5A).all())
+    assert bool((L == 0xFF).all())
