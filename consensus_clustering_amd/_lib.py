@@ -97,6 +97,8 @@ def load():
                 "`make -C consensus_clustering_amd/csrc` (hipcc --offload-arch=gfx950)")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if "CCMI_LIB" in os.environ and not hasattr(lib, name):
+                continue  # an explicitly named (older / diagnostic) build for A/B timing
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

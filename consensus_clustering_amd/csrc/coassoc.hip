@@ -46,6 +46,7 @@ namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int T = CC_TILE;            // 256
 constexpr int NT = 512;               // threads per workgroup (8 waves)
@@ -153,11 +154,12 @@ __global__ void bin_selftest_kernel(int rows, const float* __restrict__ edges,
   if (bad1) atomicAdd(&mismatches[1], bad1);
 }
 
-// Load the HS = 128/KP label bytes of one row for one super-step into w[].
+// Load the HS label bytes of one row for one super-step into w[] (HS = 128 / KP for the i8
+// kernels, 256 / KP for the FP4 kernels).
 // Branch-free: an out-of-range row reads row 0 and is masked to 0xFF (= not sampled).
-template <int KP>
+template <int HS>
 __device__ __forceinline__ void load_labels(const uint8_t* rowp, bool valid, uint32_t (&w)[32]) {
-  constexpr int HS = 128 / KP;
+  static_assert(HS >= 1 && HS <= 128, "at most 128 label bytes per row and step");
   const uint32_t msk = valid ? 0u : 0xFFFFFFFFu;
   if constexpr (HS >= 16) {
 #pragma unroll
@@ -244,6 +246,32 @@ __device__ __forceinline__ void expand_chunk(const uint32_t (&w)[32], int kc, ui
   }
 }
 
+// FP4 (e2m1) one-hot, power-of-two KP >= 4: dwords 8 kc .. 8 kc + 7 of a 256-channel super-step
+// (virtual k = h_local * KP + c, chunk kc = virtual k 64 kc .. 64 kc + 63).  Each dword holds 8
+// channels as nibbles, 0x2 = 1.0 where the label matches (products 1.0 x 1.0, f32 sums: exact
+// counts).  Nibble order inside a dword: channel 8 q + i at nibble i.  Any fixed placement is
+// valid, since the A and B operands are expanded by this same code.
+template <int KP>
+__device__ __forceinline__ void expand_chunk_f4(const uint32_t (&w)[32], int kc, uint32_t (&o)[8]) {
+  static_assert(KP >= 4 && (KP & (KP - 1)) == 0, "power-of-two KP >= 4");
+  constexpr int LOG = (KP == 4) ? 2 : (KP == 8) ? 3 : (KP == 16) ? 4 : (KP == 32) ? 5 : (KP == 64) ? 6 : 7;
+#pragma unroll
+  for (int qq = 0; qq < 8; ++qq) {
+    const int k0 = 64 * kc + 8 * qq;
+    if constexpr (KP == 4) {  // two resamples per dword (h even: same label dword)
+      const int h = k0 >> 2;
+      const uint32_t l0 = (w[h >> 2] >> (8 * (h & 3))) & 0xFFu;
+      const uint32_t l1 = (w[h >> 2] >> (8 * (h & 3) + 8)) & 0xFFu;
+      o[qq] = (l0 < 4u ? (2u << (l0 << 2)) : 0u) | (l1 < 4u ? (2u << (16u + (l1 << 2))) : 0u);
+    } else {  // one resample, channels 8 cq .. 8 cq + 7
+      const int h = k0 >> LOG;
+      const uint32_t cq = static_cast<uint32_t>((k0 & (KP - 1)) >> 3);
+      const uint32_t lab = (w[h >> 2] >> (8 * (h & 3))) & 0xFFu;
+      o[qq] = ((lab >> 3) == cq) ? (2u << ((lab & 7u) << 2)) : 0u;
+    }
+  }
+}
+
 // ---- exact-K channel packing (K not a power of two, K <= 32) -------------------------------
 // A super-step holds HS = floor(128 / K) whole resamples at virtual k = h_local * K + c, and
 // the HS*K..127 tail is zero: channels are no longer padded to the next power of two (at C3,
@@ -269,9 +297,9 @@ __device__ unsigned long long cc_co_stamp_acc[8];
 // Two load forms, chosen per K by measurement (C3, tools/gpu_co3.sh): for K < 10 aligned 16-B
 // chunks and a dword shift by selects; for K >= 10 dword-aligned 16-B loads from the dword holding
 // the first byte, so only the byte shift remains (fewer VALU where steps are many).
-template <int K>
+template <int K, int VK = 128>
 struct ExactK {
-  static constexpr int HS = 128 / K;                // resamples per super-step
+  static constexpr int HS = VK / K;                 // resamples per super-step (VK virtual k)
   static constexpr int NWX = (HS + 3) / 4;          // aligned label dwords of a step
   static constexpr bool DW = K >= 10;               // dword-aligned loads
   static constexpr int NC16 = DW ? (NWX + 1 + 3) / 4 : (HS + 15 + 15) / 16;
@@ -285,9 +313,9 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // stays in flight for a whole super-step.  No load goes past the row (the 16-B form re-reads
 // the row's last 16 bytes for a chunk at or past ldl, a multiple of 16; realign fills those
 // with 0xFF and applies the invalid-row mask).
-template <int K>
-__device__ __forceinline__ void load_raw(const uint8_t* rowp, int s, int ldl, uint32_t (&raw)[ExactK<K>::RAW]) {
-  using E = ExactK<K>;
+template <int K, int VK>
+__device__ __forceinline__ void load_raw(const uint8_t* rowp, int s, int ldl, uint32_t (&raw)[ExactK<K, VK>::RAW]) {
+  using E = ExactK<K, VK>;
   if constexpr (E::DW) {
     const int a4 = (s * E::HS) & ~3;
 #pragma unroll
@@ -323,10 +351,10 @@ __device__ __forceinline__ void load_raw(const uint8_t* rowp, int s, int ldl, ui
 // Label bytes of step s in place (byte h of w = resample s * HS + h); resamples at or past Hpad
 // (the last step's tail) read as 0xFF = not sampled.  The dword shift (16-B form) is a select on
 // the wave-uniform offset (a switch made the compiler spill), the byte shift v_alignbyte.
-template <int K>
-__device__ __forceinline__ void realign(const uint32_t (&raw_in)[ExactK<K>::RAW], int s, int Hpad, int ldl,
+template <int K, int VK>
+__device__ __forceinline__ void realign(const uint32_t (&raw_in)[ExactK<K, VK>::RAW], int s, int Hpad, int ldl,
                                         bool valid, uint32_t (&w)[32]) {
-  using E = ExactK<K>;
+  using E = ExactK<K, VK>;
   // every raw dword counts as read here: a loaded dword that realign does not need would
   // otherwise be reused as a temporary, and that write-after-load stalls on the label load
   // (issued one step ago) at the top of the next super-step instead of here
@@ -403,15 +431,84 @@ __device__ __forceinline__ void expand_chunk_exact(const uint32_t (&w)[32], int 
   }
 }
 
-template <int KP>
+// 0x80 in byte b where label(j / K) == j % K for channel j = j0 + b (j < HS K), else 0: v_perm
+// gathers the (at most two) label bytes of the 4 channels, XOR with the channel numbers, and a
+// carry-free zero-byte test.
+template <int K, int VK>
+__device__ __forceinline__ uint32_t match4(const uint32_t (&w)[32], int j0) {
+  using E = ExactK<K, VK>;
+  if (j0 >= E::HS * K) return 0u;
+  const int dA = (j0 / K) >> 2;
+  uint32_t sel = 0, cc = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int j = j0 + b;
+    const bool ok = j < E::HS * K;
+    sel |= static_cast<uint32_t>(ok ? (j / K - 4 * dA) : 0x0C) << (8 * b);
+    cc |= static_cast<uint32_t>(ok ? (j % K) : 0xFE) << (8 * b);
+  }
+  const uint32_t s1 = w[dA];
+  const uint32_t s0 = (dA + 1 < E::NWX) ? w[dA + 1] : s1;
+  const uint32_t x = __builtin_amdgcn_perm(s0, s1, sel) ^ cc;
+  const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(t | x) & 0x80808080u;
+}
+
+// FP4 exact-K one-hot: dwords 8 kc .. 8 kc + 7 of a 256-channel super-step.  Byte b of dword q
+// holds channel 8 q + b (low nibble) and 8 q + 4 + b (high nibble), 0x2 = 1.0 where it matches.
+template <int K>
+__device__ __forceinline__ void expand_chunk_exact_f4(const uint32_t (&w)[32], int kc, uint32_t (&o)[8]) {
+#pragma unroll
+  for (int qq = 0; qq < 8; ++qq) {
+    const int j0 = 8 * (8 * kc + qq);
+    o[qq] = (match4<K, 256>(w, j0) >> 6) | (match4<K, 256>(w, j0 + 4) >> 2);
+  }
+}
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+// expansion VALU interleaved per MFMA in the FP4 main loop (power-of-two / exact-K forms)
+#ifndef CO_F4_V
+#define CO_F4_V 10
+#endif
+#ifndef CO_F4_EXV
+#define CO_F4_EXV 14
+#endif
+
+// One MFMA step of the tile loop on the operand pair (a, b): i8 (32 virtual k) or FP4 (64).
+// FP4: v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 operands (format 4) and unit block scales
+// (E8M0 127 = 2^0); only the low 4 dwords of each operand are read for FP4.
+template <bool F4, class Acc>
+__device__ __forceinline__ Acc mfma_step(const v4i& a, const v4i& b, const Acc& c) {
+  if constexpr (F4) {
+    const v8i a8 = __builtin_shufflevector(a, a, 0, 1, 2, 3, -1, -1, -1, -1);
+    const v8i b8 = __builtin_shufflevector(b, b, 0, 1, 2, 3, -1, -1, -1, -1);
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 127, 0, 127);
+  } else {
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+  }
+}
+
+// Accumulator element as an unsigned count (FP4 accumulates exact integers in f32).
+__device__ __forceinline__ uint32_t count_of(int v) { return static_cast<uint32_t>(v); }
+__device__ __forceinline__ uint32_t count_of(float v) { return static_cast<uint32_t>(v); }
+
+// F4: the co-association kernels (KP >= 3) contract FP4 one-hot operands, 256 virtual k per
+// super-step (4 chunks of 64): the same LDS bytes and MFMA cycles per step as the i8 form's 128
+// virtual k, so the LDS traffic and the matrix-pipe time per count are halved.  The co-sampling
+// kernel (KP = 1, 0/1 flags of 128 resamples per step) and K <= 2 keep the i8 form.
+template <int KP, bool F4>
 __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     const uint8_t* __restrict__ labels, int n, int ldl, int Hpad, int64_t tile_begin,
     uint16_t* __restrict__ I_tiles_out, const uint16_t* __restrict__ I_tiles_in,
     const float* __restrict__ edges, unsigned long long* __restrict__ bin_counts,
     int32_t* __restrict__ full_out, const uint16_t* __restrict__ btab, int bt_rows) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-  constexpr int HS = 128 / KP;  // resamples per super-step
+  constexpr int VK = F4 ? 256 : 128;  // virtual k per super-step
+  constexpr int HS = VK / KP;  // resamples per super-step
   constexpr bool EX = (KP & (KP - 1)) != 0;  // exact-K packing (K = KP not a power of two)
+  static_assert(!F4 || KP >= 3, "FP4 form: K >= 3");
+  using Acc = std::conditional_t<F4, v16f, v16i>;
 
   CO_STAMP(st0);
   const int tid = threadIdx.x;
@@ -439,11 +536,11 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
   char* const wbase = lds + side * SIDE + erb * KC * FRAG + er * 16;
 
   const int nsteps = EX ? (Hpad + HS - 1) / HS : Hpad / HS;
-  v16i acc[4][2];
+  Acc acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = v16i{};
+    for (int j = 0; j < 2; ++j) acc[i][j] = Acc{};
 
   // Label prefetch depth: two steps ahead for the co-association kernels (<= 16 label bytes
   // per row and step); the co-sampling kernel (128 bytes per row and step) loads one step
@@ -451,39 +548,60 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
   constexpr bool PF2 = KP > 1;
   constexpr int NWD = (HS + 3) / 4;
   uint32_t w[32], wn[PF2 ? NWD : 1], o[32];
-  constexpr int NRW = EX ? ExactK<EX ? KP : 3>::RAW : 1;
+  constexpr int KX = EX ? KP : 3;  // (a valid instantiation when unused)
+  constexpr int NRW = EX ? ExactK<KX, VK>::RAW : 1;
   uint32_t raw1[NRW];  // exact K: raw chunks of step s+2 (one step in flight; two measured slower)
-  if constexpr (EX) {
-    load_raw<KP>(rowp, 0, ldl, raw1);
-    realign<KP>(raw1, 0, Hpad, ldl, evalid, w);
+  // the one-hot dwords of chunk kc of the step whose labels are in w
+  auto expand_kc = [&](int kc, uint32_t (&oc)[8]) __attribute__((always_inline)) {
+    if constexpr (EX && F4)
+      expand_chunk_exact_f4<KX>(w, kc, oc);
+    else if constexpr (EX)
+      expand_chunk_exact<KX>(w, kc, oc);
+    else if constexpr (F4)
+      expand_chunk_f4<(KP >= 4 ? KP : 4)>(w, kc, oc);
+    else
+      expand_chunk<KP>(w, kc, oc);
+  };
+  // step 0's one-hot straight into LDS buffer 0, chunk by chunk
+  auto store_step0 = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       uint32_t oc[8];
-      expand_chunk_exact<KP>(w, kc, oc);
+      expand_kc(kc, oc);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) o[8 * kc + q] = oc[q];
+      for (int g = 0; g < 2; ++g)
+        *reinterpret_cast<uint4*>(wbase + kc * FRAG + g * 512) =
+            make_uint4(oc[g * 4 + 0], oc[g * 4 + 1], oc[g * 4 + 2], oc[g * 4 + 3]);
     }
-    load_raw<KP>(rowp, nsteps > 1 ? 1 : 0, ldl, raw1);
-    realign<KP>(raw1, nsteps > 1 ? 1 : 0, Hpad, ldl, evalid, w);  // step 1
-    load_raw<KP>(rowp, nsteps > 2 ? 2 : 0, ldl, raw1);  // step 2
+  };
+  if constexpr (EX) {
+    load_raw<KX, VK>(rowp, 0, ldl, raw1);
+    realign<KX, VK>(raw1, 0, Hpad, ldl, evalid, w);
+    store_step0();
+    load_raw<KX, VK>(rowp, nsteps > 1 ? 1 : 0, ldl, raw1);
+    realign<KX, VK>(raw1, nsteps > 1 ? 1 : 0, Hpad, ldl, evalid, w);  // step 1
+    load_raw<KX, VK>(rowp, nsteps > 2 ? 2 : 0, ldl, raw1);  // step 2
+  } else if constexpr (PF2) {
+    load_labels<HS>(rowp, evalid, w);
+    store_step0();
   } else {
-    load_labels<KP>(rowp, evalid, w);
+    load_labels<HS>(rowp, evalid, w);
     expand<KP>(w, o);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+        *reinterpret_cast<uint4*>(wbase + kc * FRAG + g * 512) =
+            make_uint4(o[kc * 8 + g * 4 + 0], o[kc * 8 + g * 4 + 1], o[kc * 8 + g * 4 + 2],
+                       o[kc * 8 + g * 4 + 3]);
   }
   if constexpr (PF2 && !EX) {
-    load_labels<KP>(rowp + (nsteps > 1 ? HS : 0), evalid, w);  // step 1
+    load_labels<HS>(rowp + (nsteps > 1 ? HS : 0), evalid, w);  // step 1
     uint32_t t32[32];
-    load_labels<KP>(rowp + (nsteps > 2 ? 2 * HS : 0), evalid, t32);  // step 2
+    load_labels<HS>(rowp + (nsteps > 2 ? 2 * HS : 0), evalid, t32);  // step 2
 #pragma unroll
     for (int q = 0; q < NWD; ++q) wn[q] = t32[q];
   }
-#pragma unroll
-  for (int kc = 0; kc < KC; ++kc)
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-      *reinterpret_cast<uint4*>(wbase + kc * FRAG + g * 512) =
-          make_uint4(o[kc * 8 + g * 4 + 0], o[kc * 8 + g * 4 + 1], o[kc * 8 + g * 4 + 2],
-                     o[kc * 8 + g * 4 + 3]);
   __syncthreads();
   CO_STAMP(st1);
   CO_ACC(0, st0, st1);
@@ -493,7 +611,7 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     const char* rb = lds + (s & 1) * BUF;
     char* wb = wbase + ((s + 1) & 1) * BUF;
     if constexpr (!PF2)
-      if (more) load_labels<KP>(rowp + (s + 1) * HS, evalid, w);
+      if (more) load_labels<HS>(rowp + (s + 1) * HS, evalid, w);
     // operand fragments double-buffered across the k-chunks: the reads of chunk kc+1 are in
     // flight while chunk kc's MFMAs issue (only the first chunk's read latency is exposed)
     v4i a[2][4], b[2][2];
@@ -516,17 +634,14 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int nj = 0; nj < 2; ++nj)
-          acc[mi][nj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[cb][mi], b[cb][nj], acc[mi][nj], 0, 0, 0);
+          acc[mi][nj] = mfma_step<F4>(a[cb][mi], b[cb][nj], acc[mi][nj]);
       if constexpr (PF2) {
         // one-hot expansion of step s+1 (labels prefetched two steps ahead) interleaved with
         // this step's MFMAs: chunk kc's 8 dwords are expanded and stored right after chunk
         // kc's MFMAs issue, so the vector work runs in the MFMA shadows
         // (the stores are unconditional: on the last step they land in the buffer nobody reads)
         uint32_t oc[8];
-        if constexpr (EX)
-          expand_chunk_exact<KP>(w, kc, oc);
-        else
-          expand_chunk<KP>(w, kc, oc);
+        expand_kc(kc, oc);
 #pragma unroll
         for (int g = 0; g < 2; ++g)
           *reinterpret_cast<uint4*>(wb + kc * FRAG + g * 512) =
@@ -536,21 +651,21 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, (EX && KP >= 10) ? 9 : 6, 0);  // VALU per MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, F4 ? (EX ? CO_F4_EXV : CO_F4_V) : ((EX && KP >= 10) ? 9 : 6), 0);  // VALU per MFMA
         }
         __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);    // the 2 LDS stores
       }
     }
     if constexpr (EX) {
       // w <- step s+2 (loaded one step ago), raw1 <- step s+3
-      realign<KP>(raw1, (s + 2) < nsteps ? s + 2 : s, Hpad, ldl, evalid, w);
-      load_raw<KP>(rowp, (s + 3) < nsteps ? s + 3 : s, ldl, raw1);
+      realign<KX, VK>(raw1, (s + 2) < nsteps ? s + 2 : s, Hpad, ldl, evalid, w);
+      load_raw<KX, VK>(rowp, (s + 3) < nsteps ? s + 3 : s, ldl, raw1);
     } else if constexpr (PF2) {
       // rotate the label prefetch: w <- step s+2, wn <- step s+3 (clamped re-reads at the end)
 #pragma unroll
       for (int q = 0; q < NWD; ++q) w[q] = wn[q];
       uint32_t t32[32];
-      load_labels<KP>(rowp + ((s + 3) < nsteps ? s + 3 : s) * HS, evalid, t32);
+      load_labels<HS>(rowp + ((s + 3) < nsteps ? s + 3 : s) * HS, evalid, t32);
 #pragma unroll
       for (int q = 0; q < NWD; ++q) wn[q] = t32[q];
     } else if (more) {
@@ -656,7 +771,7 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           uint32_t lo[16], hi[16];
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
-            const uint32_t m = static_cast<uint32_t>(acc[mi][nj][v]);
+            const uint32_t m = count_of(acc[mi][nj][v]);
             g[v] = static_cast<int>(static_cast<float>(m) * rc[v]);
             g[v] = g[v] > NBINS - 1 ? NBINS - 1 : g[v];
             const uint16_t* row = tab + ival[v] * BT_ROW;
@@ -667,7 +782,7 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(lo[v]), "+v"(hi[v]));
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
-            const uint32_t m = static_cast<uint32_t>(acc[mi][nj][v]);
+            const uint32_t m = count_of(acc[mi][nj][v]);
             const int b = g[v] - (m < lo[v] ? 1 : 0) + (m >= hi[v] ? 1 : 0);
             atomicAdd(&hist[b * NT + tid], 1u);
           }
@@ -682,7 +797,7 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
           const uint32_t ival = (iw[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
-          const int val = acc[mi][nj][v];
+          const int val = static_cast<int>(count_of(acc[mi][nj][v]));
           const int i = row0 + mi * 32 + (v & 3) + 8 * (v >> 2);
           const int j = col0 + nj * 32;
           if (i < j && j < n) {
@@ -788,12 +903,12 @@ int launch_status(const char* fn) {
   return CC_OK;
 }
 
-template <int KP>
+template <int KP, bool F4 = false>
 void launch_tiles(dim3 grid, hipStream_t st, const uint8_t* lab, int n, int ldl, int Hpad,
                   int64_t tb, uint16_t* Iout, const uint16_t* Iin, const float* edges,
                   unsigned long long* counts, int32_t* full, const uint16_t* btab = nullptr,
                   int bt_rows = 0) {
-  hipLaunchKernelGGL(tiles_kernel<KP>, grid, dim3(NT), 0, st, lab, n, ldl, Hpad, tb, Iout, Iin,
+  hipLaunchKernelGGL((tiles_kernel<KP, F4>), grid, dim3(NT), 0, st, lab, n, ldl, Hpad, tb, Iout, Iin,
                      edges, counts, full, btab, bt_rows);
 }
 
@@ -909,31 +1024,30 @@ extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int
   const dim3 grid(static_cast<unsigned>(ntl));
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const uint8_t* lab = reinterpret_cast<const uint8_t*>(labels_nh);
-  int kp = 2;
+  // K <= 2: i8 one-hot (KP = 2, 64 resamples per step).  K >= 3: FP4 one-hot, 256 virtual k
+  // per step, channels padded to the next power of two KP >= 4, or exact-K packing (ExactK)
+  // where it saves at least 40 % of the super-steps (K = 17, 18 at Hpad = 1024).  Measured at
+  // C3 (tools/co_only.py): the exact form's expansion costs more VALU per step, and at K < 17
+  // its register demand spills, so K = 5, 9, 10, 11, 19, 20 ran 5-100 % slower exact than padded.
+  // CCMI_CO_PACK=pow2 / exact forces one form where both exist (diagnostics; identical counts).
+  int kp = K <= 2 ? 2 : 4;
   while (kp < K) kp <<= 1;
-  // Exact-K packing (ExactK) when it saves enough super-steps: its expansion costs more VALU
-  // per step than the power-of-two form.  CCMI_CO_PACK=pow2 / exact forces one form
-  // (diagnostics; both give identical counts).
   if (kp != K && K < 32) {
-    const int hs = 128 / K, se = (Hpad + hs - 1) / hs, sp = Hpad / (128 / kp);
+    const int hs = 256 / K, se = (Hpad + hs - 1) / hs, sp = Hpad / (256 / kp);
     const char* pk = std::getenv("CCMI_CO_PACK");
     const bool force_pow2 = pk && pk[0] == 'p', force_exact = pk && pk[0] == 'e';
-    if (force_exact || (!force_pow2 && 4 * se < 3 * sp)) kp = K;
+    if (force_exact || (!force_pow2 && 5 * se <= 3 * sp && K >= 17)) kp = K;
   }
   switch (kp) {
-#define CC_EXACT(k) case k: launch_tiles<k>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+#define CC_EXACT(k) case k: launch_tiles<k, true>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
     CC_EXACT(3) CC_EXACT(5) CC_EXACT(6) CC_EXACT(7) CC_EXACT(9) CC_EXACT(10) CC_EXACT(11)
     CC_EXACT(12) CC_EXACT(13) CC_EXACT(14) CC_EXACT(15) CC_EXACT(17) CC_EXACT(18) CC_EXACT(19)
     CC_EXACT(20) CC_EXACT(21) CC_EXACT(22) CC_EXACT(23) CC_EXACT(24) CC_EXACT(25) CC_EXACT(26)
     CC_EXACT(27) CC_EXACT(28) CC_EXACT(29) CC_EXACT(30) CC_EXACT(31)
+    CC_EXACT(4) CC_EXACT(8) CC_EXACT(16) CC_EXACT(32) CC_EXACT(64)
 #undef CC_EXACT
     case 2: launch_tiles<2>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
-    case 4: launch_tiles<4>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
-    case 8: launch_tiles<8>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
-    case 16: launch_tiles<16>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
-    case 32: launch_tiles<32>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
-    case 64: launch_tiles<64>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
-    default: launch_tiles<128>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    default: launch_tiles<128, true>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
   }
   return launch_status("cc_coassoc");
 }

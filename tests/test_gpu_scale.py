@@ -10,16 +10,20 @@ For each config the drop-in fit runs at the real n, d, K range and H, then:
     labels: the co-sampling tile (diagonal = per-row sample counts) and the 20 histogram
     counts of every K must be bit-identical to the GPU's (CC.py:264, :287-290, :338-344);
   * C2 / C3: the k-means labels of the first resamples at the full m equal sklearn's
-    KMeans (the reference's clusterer, CC.py:282) for every K <= the true number of blobs.
+    KMeans (the reference's clusterer, CC.py:282) for every K <= the true number of blobs, and
+    for further resamples over the WHOLE K range every disagreement with sklearn's float32
+    fit is a problem where sklearn's own float32 and float64 fits disagree (sk_parity);
+  * C4: the wide engine on the gene-expression-like rows, the same checks.
 C2 (n = 10k) also keeps the full matrices: iij and mij are compared with the oracle's.
 """
 import numpy as np
 import pytest
 import torch
 
-from bench import CONFIGS, SEED, make_blobs_f32
+from bench import CONFIGS, SEED, make_blobs_f32, make_expression_f32
 from consensus_clustering_amd import engine, post
 from oracle import cc_oracle as O
+from tests.sk_parity import sklearn_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -79,7 +83,10 @@ def fit_config(name, keep=False):
     from consensus_clustering_amd import ConsensusClustering
 
     cfg = CONFIGS[name]
-    X = make_blobs_f32(cfg["n"], cfg["d"], cfg["k_true"], seed=SEED)
+    if cfg.get("data") == "expression":
+        X = make_expression_f32(cfg["n"], cfg["d"], groups=cfg["k_true"], seed=SEED)
+    else:
+        X = make_blobs_f32(cfg["n"], cfg["d"], cfg["k_true"], seed=SEED)
     cc = ConsensusClustering(K_range=cfg["Ks"], n_iterations=cfg["H"], subsampling=cfg["frac"],
                              random_state=SEED, plot_cdf=False, keep_matrices=keep)
     cc.fit(torch.from_numpy(X).to(engine.require_gpu()))
@@ -163,12 +170,24 @@ def check_kmeans(cfg, X, cc, resamples):
                 assert np.array_equal(ref, got), (K, h, float(np.mean(ref == got)))
 
 
+def test_c4_full_size():
+    """BASELINE config 4 (gene-expression-like rows, n = 5k x d = 20k, K = 2..12, H = 1000) at
+    full size through the wide engine: pair-count sums, label columns, oracle-checked tiles, and
+    sklearn's labels for one resample of every K."""
+    cfg, X, cc = fit_config("c4")
+    check_counts_sum(cfg, cc)
+    check_labels(cfg, cc)
+    check_tiles(cfg, cc, Ks_check=[2, 5, 12])
+    sklearn_parity(X, cc.labels_, cc.resampling_indices_, cfg["Ks"], SEED, resamples=1)
+
+
 def test_c3_full_size():
     cfg, X, cc = fit_config("c3")
     check_counts_sum(cfg, cc)
     check_labels(cfg, cc)
     check_tiles(cfg, cc, Ks_check=[2, 8, 13, 20])
     check_kmeans(cfg, X, cc, resamples=2)
+    sklearn_parity(X, cc.labels_, cc.resampling_indices_, cfg["Ks"], SEED, resamples=1, skip=2)
 
 
 def test_c5_full_size():
@@ -183,6 +202,7 @@ def test_c2_full_size_with_matrices():
     check_counts_sum(cfg, cc)
     check_labels(cfg, cc)
     check_kmeans(cfg, X, cc, resamples=3)
+    sklearn_parity(X, cc.labels_, cc.resampling_indices_, cfg["Ks"], SEED, resamples=2, skip=3)
     n = cfg["n"]
     idx = cc.resampling_indices_.astype(np.int64)
     I_ref = O.cosample_matrix(idx, n)
