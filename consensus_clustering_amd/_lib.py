@@ -33,8 +33,10 @@ SIGNATURES = {
     "cc_cosample": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp]),
     "cc_coassoc": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp,
                             _vp, _vp, _c_int, _vp]),
-    "cc_bin_table": (_c_int, [_c_int, _vp, _vp, _vp]),
+    "cc_bin_table": (_c_int, [_c_int, _vp, _vp, _c_sz, _vp]),
+    "cc_bin_table_bytes": (_c_sz, [_c_int]),
     "cc_bin_table_max_rows": (_c_int, []),
+    "cc_bin_table_form_rows": (_c_int, [_c_int]),
     "cc_consensus": (_c_int, [_vp, _vp, _c_int, _vp, _vp]),
     "cc_kmeans_plan": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int]),
     "cc_kmeans_workspace_bytes": (_c_sz, [_c_int, _c_int, _vp, _c_int, _c_int, _c_int]),

@@ -104,7 +104,8 @@ class ConsensusClustering:
         self.device = device
         self.workspace_budget = workspace_budget
         # k-means arithmetic: 'f64' = float64 like sklearn on float64 input (cc_kmeans_f64),
-        # 'fast' = the float32-class f16 hi/lo MFMA engine; 'auto' picks by the input dtype
+        # 'fast' = the float32-class f16 hi/lo MFMA engine; 'auto' = f64 for float64 input while
+        # the float64 engine's work is small (F64_AUTO_MAX_WORK), else fast with a warning
         self.precision = precision
         # where the resample indices are drawn: 'device' (cc_resample_device, n <= 65536),
         # 'host' (native threads, then uploaded), 'auto' = device when n allows; identical draws
@@ -216,7 +217,20 @@ class ConsensusClustering:
         self.backend_ = 'gpu-kmeans' if km is not None else 'host-clusterer'
         precision = self.precision
         if precision == 'auto':
-            precision = 'f64' if wdtype == np.float64 else 'fast'
+            precision = 'fast'
+            if wdtype == np.float64 and km is not None:
+                # float64 input: the reference's clusterer runs in float64 (CC.py:282), which
+                # cc_kmeans_f64 reproduces, but at ~40x the fast engine's time (one workgroup
+                # per (resample, K); 4.2 s per C3 resample against 0.11 s,
+                # profiles/r03/f64_vs_fast_c3_H4.txt): take it only while it stays small
+                work = float(H) * m * X.shape[1] * sum(Ks) * km["n_init"]
+                if work <= self.F64_AUTO_MAX_WORK:
+                    precision = 'f64'
+                else:
+                    warnings.warn(
+                        f"float64 input: the float64 k-means would take ~{work * 1.3e-9:.0f} s here; "
+                        "using the float32-class engine (precision='fast'); pass precision='f64' "
+                        "to force sklearn's float64 arithmetic")
         if precision not in ('f64', 'fast'):
             raise ValueError("precision must be 'auto', 'f64' or 'fast'")
         self.precision_ = precision if km is not None else None
@@ -365,6 +379,10 @@ class ConsensusClustering:
             del mm
             out[K] = path
         return out
+
+    # precision='auto' on float64 input: the float64 k-means while H m d sum(K) n_init stays at
+    # or below this (about 1 s of cc_kmeans_f64 at the measured ~1.3 ns per unit; C1 is 1.1e7)
+    F64_AUTO_MAX_WORK = 7.5e8
 
     # largest n for predict(): the linkage runs on the host over the n x n float64 distances
     PREDICT_MAX_N = 20000

@@ -34,6 +34,7 @@
 // workgroup and added to 20 uint64 global counters (integer atomics: order-free).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cmath>
 #include <cstdlib>
@@ -59,9 +60,34 @@ constexpr int NBINS = CC_NBINS;
 constexpr int NW = NT / 64;
 // epilogue LDS: hist [NBINS][NT] u32 | 32 edges f32 | wave sums [NBINS][NW] u32 | bin table
 constexpr int BT_OFF = NBINS * NT * 4 + 32 * 4 + NBINS * NW * 4;
-// staged table: rows x 21 uint16 thresholds, then (16-B aligned) rows x f32 reciprocals 20/i
-constexpr int BT_MAX_ROWS = (LDS_BYTES - BT_OFF - 32) / ((NBINS + 1) * 2 + 4);
+// The on-chip binning table, staged per tile in one of three forms (chosen by the row count,
+// i.e. by H):
+//   TRI  (rows <= BT_TRI_ROWS, H <= ~420): the bin itself, one byte per (m <= i) pair at
+//        i (i + 1) / 2 + m: one LDS read per element;
+//   PAIR (rows <= BT_PAIR_ROWS, H <= ~1060): per row 20 uint32 threshold pairs
+//        T[g] | T[g + 1] << 16 and the reciprocal 20 / i: two LDS reads per element;
+//   U16  (rows <= BT_MAX_ROWS): per row 21 uint16 thresholds and the reciprocal: three.
+// cc_bin_table writes every form that fits into one global buffer (u16 part first, then the
+// pair part, then the triangle), so each tile copies its form with 16-B loads.
+constexpr int BT_AVAIL = LDS_BYTES - BT_OFF - 32;
+constexpr int BT_MAX_ROWS = BT_AVAIL / ((NBINS + 1) * 2 + 4);
+constexpr int BT_PAIR_ROWS = (BT_AVAIL - 16) / (NBINS * 4 + 4);
+constexpr int bt_tri_rows() {
+  int r = 1;
+  while ((static_cast<int64_t>(r + 1) * (r + 2) / 2 + 15) / 16 * 16 <= BT_AVAIL) ++r;
+  return r;
+}
+constexpr int BT_TRI_ROWS = bt_tri_rows();
 static_assert(BT_OFF % 16 == 0, "table copies are 16-B");
+enum { BT_U16 = 0, BT_PAIR = 1, BT_TRI = 2 };
+__host__ __device__ constexpr int bt_form(int rows) {
+  return rows <= BT_TRI_ROWS ? BT_TRI : (rows <= BT_PAIR_ROWS ? BT_PAIR : BT_U16);
+}
+__host__ __device__ constexpr int64_t bt_u16_bytes(int rows) { return (static_cast<int64_t>(rows) * (NBINS + 1) * 2 + 15) / 16 * 16; }
+__host__ __device__ constexpr int64_t bt_pair_bytes(int rows) { return rows <= BT_PAIR_ROWS ? static_cast<int64_t>(rows) * NBINS * 4 : 0; }
+__host__ __device__ constexpr int64_t bt_tri_bytes(int rows) {
+  return rows <= BT_TRI_ROWS ? (static_cast<int64_t>(rows) * (rows + 1) / 2 + 15) / 16 * 16 : 0;
+}
 
 __device__ __forceinline__ void tile_coords(int64_t t, int nb, int& bi, int& bj) {
   auto start = [nb](int64_t b) -> int64_t { return b * nb - b * (b - 1) / 2; };
@@ -132,9 +158,44 @@ __global__ void bin_table_kernel(int rows, const float* __restrict__ edges, uint
   table[e] = static_cast<uint16_t>(t);
 }
 
+// The bin of (m, i) from the threshold-pair form: P[i][g] = T[g] | T[g + 1] << 16.
+__device__ __forceinline__ int pair_bin(uint32_t m, uint32_t i, const uint32_t* pair, const float* rtab) {
+  int g = static_cast<int>(static_cast<float>(m) * rtab[i]);
+  g = g > NBINS - 1 ? NBINS - 1 : g;
+  const uint32_t pr = pair[i * NBINS + g];
+  return g - (m < (pr & 0xFFFFu) ? 1 : 0) + (m >= (pr >> 16) ? 1 : 0);
+}
+
+// The bin of (m <= i) from the triangle form.
+__device__ __forceinline__ int tri_bin(uint32_t m, uint32_t i, const uint8_t* tri) {
+  return tri[((i * (i + 1)) >> 1) + m];
+}
+
+// pair and triangle forms from the u16 thresholds (cc_bin_table, after bin_table_kernel)
+__global__ void bin_table_pack_kernel(int rows, uint16_t* __restrict__ table) {
+  const uint16_t* t16 = table;
+  uint32_t* pair = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + bt_u16_bytes(rows));
+  uint8_t* tri = reinterpret_cast<uint8_t*>(table) + bt_u16_bytes(rows) + bt_pair_bytes(rows);
+  const int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (bt_pair_bytes(rows) && e < static_cast<int64_t>(rows) * NBINS) {
+    const int i = static_cast<int>(e / NBINS), g = static_cast<int>(e - static_cast<int64_t>(i) * NBINS);
+    pair[e] = static_cast<uint32_t>(t16[i * BT_ROW + g]) | (static_cast<uint32_t>(t16[i * BT_ROW + g + 1]) << 16);
+  }
+  if (bt_tri_bytes(rows) && e < static_cast<int64_t>(rows) * (rows + 1) / 2) {
+    int i = static_cast<int>((sqrt(8.0 * static_cast<double>(e) + 1.0) - 1.0) * 0.5);
+    while (static_cast<int64_t>(i) * (i + 1) / 2 > e) --i;
+    while (static_cast<int64_t>(i + 1) * (i + 2) / 2 <= e) ++i;
+    const uint32_t m = static_cast<uint32_t>(e - static_cast<int64_t>(i) * (i + 1) / 2);
+    int b = 0;
+    for (int k = 1; k < NBINS; ++k) b += m >= t16[i * BT_ROW + k] ? 1 : 0;
+    tri[e] = static_cast<uint8_t>(b);
+  }
+}
+
 // Exhaustive check of the division-free binning: for every pair (m <= i < rows) compare
-// table_bin and table_bin_r (with the epilogue's own reciprocal 20 * rcp(i)) against the direct
-// numpy-exact consensus_bin; mismatches[0] / [1] count the disagreements of the two forms.
+// table_bin and table_bin_r (with the epilogue's own reciprocal 20 * rcp(i)) and, where the
+// table holds them, the pair and triangle forms, against the direct numpy-exact consensus_bin;
+// mismatches[0..3] count the disagreements of the four forms.
 __global__ void bin_selftest_kernel(int rows, const float* __restrict__ edges,
                                     const uint16_t* __restrict__ table,
                                     unsigned long long* __restrict__ mismatches) {
@@ -143,15 +204,21 @@ __global__ void bin_selftest_kernel(int rows, const float* __restrict__ edges,
   __shared__ float rtab_i[1];
   if (threadIdx.x == 0) rtab_i[0] = rt;
   __syncthreads();
-  unsigned long long bad0 = 0, bad1 = 0;
+  const uint32_t* pair = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + bt_u16_bytes(rows));
+  const uint8_t* tri = reinterpret_cast<const uint8_t*>(table) + bt_u16_bytes(rows) + bt_pair_bytes(rows);
+  unsigned long long bad0 = 0, bad1 = 0, bad2 = 0, bad3 = 0;
   for (int m = threadIdx.x; m <= i; m += blockDim.x) {
     const int want = consensus_bin(static_cast<uint32_t>(m), static_cast<uint32_t>(i), edges);
     bad0 += table_bin(static_cast<uint32_t>(m), static_cast<uint32_t>(i), table) != want;
-    // table_bin_r reads rtab[i]: point it at a one-entry array holding row i's reciprocal
+    // table_bin_r / pair_bin read rtab[i]: point it at a one-entry array holding row i's reciprocal
     bad1 += table_bin_r(static_cast<uint32_t>(m), static_cast<uint32_t>(i), table, rtab_i - i) != want;
+    if (bt_pair_bytes(rows)) bad2 += pair_bin(static_cast<uint32_t>(m), static_cast<uint32_t>(i), pair, rtab_i - i) != want;
+    if (bt_tri_bytes(rows)) bad3 += tri_bin(static_cast<uint32_t>(m), static_cast<uint32_t>(i), tri) != want;
   }
   if (bad0) atomicAdd(&mismatches[0], bad0);
   if (bad1) atomicAdd(&mismatches[1], bad1);
+  if (bad2) atomicAdd(&mismatches[2], bad2);
+  if (bad3) atomicAdd(&mismatches[3], bad3);
 }
 
 // Load the HS label bytes of one row for one super-step into w[] (HS = 128 / KP for the i8
@@ -729,26 +796,88 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     uint32_t* hist = reinterpret_cast<uint32_t*>(lds);
     float* es = reinterpret_cast<float*>(lds + NBINS * NT * sizeof(uint32_t));
     uint16_t* tab = reinterpret_cast<uint16_t*>(lds + BT_OFF);
+    const uint32_t* ptab = reinterpret_cast<const uint32_t*>(lds + BT_OFF);
+    const uint8_t* ttab = reinterpret_cast<const uint8_t*>(lds + BT_OFF);
+    const int form = bt_form(bt_rows);  // launch-uniform
+    // the staged form's bytes and where it sits in the global table; the reciprocals follow it
+    const int64_t fbytes = form == BT_TRI ? bt_tri_bytes(bt_rows)
+                                          : (form == BT_PAIR ? bt_pair_bytes(bt_rows) : bt_u16_bytes(bt_rows));
+    const int64_t fsrc = form == BT_TRI ? bt_u16_bytes(bt_rows) + bt_pair_bytes(bt_rows)
+                                        : (form == BT_PAIR ? bt_u16_bytes(bt_rows) : 0);
 #pragma unroll
     for (int b = 0; b < NBINS; ++b) hist[b * NT + tid] = 0;
     if (tid <= NBINS) es[tid] = edges[tid];
-    if (btab) {  // 16-B copies (the table allocation is padded to 16 B)
-      const int vecs = (bt_rows * BT_ROW * 2 + 15) / 16;
-      const uint4* src = reinterpret_cast<const uint4*>(btab);
+    float* rtab_w = reinterpret_cast<float*>(lds + BT_OFF + fbytes);
+    if (btab) {  // 16-B copies (every form is a multiple of 16 B)
+      const int vecs = static_cast<int>(fbytes / 16);
+      const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(btab) + fsrc);
       uint4* dst = reinterpret_cast<uint4*>(tab);
       for (int e = tid; e < vecs; e += NT) dst[e] = src[e];
-      float* rtab = reinterpret_cast<float*>(lds + BT_OFF + 16 * vecs);
-      for (int r = tid; r < bt_rows; r += NT)
-        rtab[r] = r > 0 ? 20.0f * __builtin_amdgcn_rcpf(static_cast<float>(r)) : 0.0f;
+      if (form != BT_TRI)
+        for (int r = tid; r < bt_rows; r += NT)
+          rtab_w[r] = r > 0 ? 20.0f * __builtin_amdgcn_rcpf(static_cast<float>(r)) : 0.0f;
     }
     __syncthreads();
     CO_STAMP(st3);
     CO_ACC(2, st2, st3);
-    const float* rtab = reinterpret_cast<const float*>(lds + BT_OFF + 16 * ((bt_rows * BT_ROW * 2 + 15) / 16));
+    const float* rtab = rtab_w;
     const uint4* it4 = reinterpret_cast<const uint4*>(I_tiles_in + tl * (T * T) + 128 * tid);
     // Interior tiles (off the diagonal, every column < n; all but a sliver of the triangle)
-    // bin every element with no pair mask, through the staged reciprocal table.
-    if (btab && !diag && (bj + 1) * T <= n && !full_out) {
+    // bin every element with no pair mask, through the staged table: batched LDS passes per
+    // block of 16 elements (all reads of a pass in flight together, then the counter adds).
+    const bool interior = btab && !diag && (bj + 1) * T <= n && !full_out;
+    if (interior && form == BT_TRI) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) {
+          const uint4 q0 = it4[(mi * 2 + nj) * 2], q1 = it4[(mi * 2 + nj) * 2 + 1];
+          const uint32_t iw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+          uint32_t bb[16];
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const uint32_t iv = (iw[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
+            bb[v] = tri_bin(count_of(acc[mi][nj][v]), iv, ttab);
+          }
+#pragma unroll
+          for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(bb[v]));
+#pragma unroll
+          for (int v = 0; v < 16; ++v) atomicAdd(&hist[bb[v] * NT + tid], 1u);
+        }
+    } else if (interior && form == BT_PAIR) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) {
+          const uint4 q0 = it4[(mi * 2 + nj) * 2], q1 = it4[(mi * 2 + nj) * 2 + 1];
+          const uint32_t iw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+          uint32_t ival[16];
+          float rc[16];
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            ival[v] = (iw[v >> 1] >> (16 * (v & 1))) & 0xFFFFu;
+            rc[v] = rtab[ival[v]];
+          }
+#pragma unroll
+          for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(rc[v]));
+          int g[16];
+          uint32_t pr[16];
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            g[v] = static_cast<int>(acc[mi][nj][v] * rc[v]);  // the accumulator is the exact count
+            g[v] = g[v] > NBINS - 1 ? NBINS - 1 : g[v];
+            pr[v] = ptab[ival[v] * NBINS + g[v]];
+          }
+#pragma unroll
+          for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(pr[v]));
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const uint32_t m = count_of(acc[mi][nj][v]);
+            const int b = g[v] - (m < (pr[v] & 0xFFFFu) ? 1 : 0) + (m >= (pr[v] >> 16) ? 1 : 0);
+            atomicAdd(&hist[b * NT + tid], 1u);
+          }
+        }
+    } else if (interior) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -801,8 +930,10 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           const int i = row0 + mi * 32 + (v & 3) + 8 * (v >> 2);
           const int j = col0 + nj * 32;
           if (i < j && j < n) {
-            const int b = btab ? table_bin(static_cast<uint32_t>(val), ival, tab)
-                               : consensus_bin(static_cast<uint32_t>(val), ival, es);
+            const int b = !btab ? consensus_bin(static_cast<uint32_t>(val), ival, es)
+                        : form == BT_TRI ? tri_bin(static_cast<uint32_t>(val), ival, ttab)
+                        : form == BT_PAIR ? pair_bin(static_cast<uint32_t>(val), ival, ptab, rtab)
+                                          : table_bin(static_cast<uint32_t>(val), ival, tab);
             atomicAdd(&hist[b * NT + tid], 1u);
           }
           if (full_out && i < n && j < n) {
@@ -972,18 +1103,33 @@ extern "C" int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, in
 }
 
 // table: rows * 21 uint16, allocated to a multiple of 16 B (cc_coassoc copies it in 16-B pieces)
-extern "C" int cc_bin_table(int rows, const float* edges, uint16_t* table, void* stream) {
-  if (rows <= 0 || rows > BT_MAX_ROWS || !edges || !table) {
-    cc::set_error("cc_bin_table: bad arguments (1 <= rows <= cc_bin_table_max_rows())");
+extern "C" size_t cc_bin_table_bytes(int rows) {
+  if (rows <= 0 || rows > BT_MAX_ROWS) return 0;
+  return static_cast<size_t>(bt_u16_bytes(rows) + bt_pair_bytes(rows) + bt_tri_bytes(rows));
+}
+
+extern "C" int cc_bin_table(int rows, const float* edges, uint16_t* table, size_t table_bytes, void* stream) {
+  if (rows <= 0 || rows > BT_MAX_ROWS || !edges || !table || table_bytes < cc_bin_table_bytes(rows)) {
+    cc::set_error("cc_bin_table: bad arguments (1 <= rows <= cc_bin_table_max_rows(), "
+                  "table_bytes >= cc_bin_table_bytes(rows))");
     return CC_ERR_ARG;
   }
+  const hipStream_t st = static_cast<hipStream_t>(stream);
   const int total = rows * BT_ROW;
-  hipLaunchKernelGGL(bin_table_kernel, dim3((total + 255) / 256), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), rows, edges, table);
+  hipLaunchKernelGGL(bin_table_kernel, dim3((total + 255) / 256), dim3(256), 0, st, rows, edges, table);
+  const int64_t packed = std::max<int64_t>(bt_pair_bytes(rows) ? static_cast<int64_t>(rows) * NBINS : 0,
+                                           bt_tri_bytes(rows) ? static_cast<int64_t>(rows) * (rows + 1) / 2 : 0);
+  if (packed > 0)
+    hipLaunchKernelGGL(bin_table_pack_kernel, dim3(static_cast<unsigned>((packed + 255) / 256)), dim3(256), 0, st,
+                       rows, table);
   return launch_status("cc_bin_table");
 }
 
 extern "C" int cc_bin_table_max_rows(void) { return BT_MAX_ROWS; }
+
+extern "C" int cc_bin_table_form_rows(int form) {
+  return form == BT_TRI ? BT_TRI_ROWS : (form == BT_PAIR ? BT_PAIR_ROWS : (form == BT_U16 ? BT_MAX_ROWS : 0));
+}
 
 extern "C" int cc_bin_selftest(int rows, const float* edges, const uint16_t* table,
                                unsigned long long* mismatches, void* stream) {
@@ -1025,27 +1171,24 @@ extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int
   const hipStream_t st = static_cast<hipStream_t>(stream);
   const uint8_t* lab = reinterpret_cast<const uint8_t*>(labels_nh);
   // K <= 2: i8 one-hot (KP = 2, 64 resamples per step).  K >= 3: FP4 one-hot, 256 virtual k
-  // per step, channels padded to the next power of two KP >= 4, or exact-K packing (ExactK)
-  // where it saves at least 40 % of the super-steps (K = 17, 18 at Hpad = 1024).  Measured at
-  // C3 (tools/co_only.py): the exact form's expansion costs more VALU per step, and at K < 17
-  // its register demand spills, so K = 5, 9, 10, 11, 19, 20 ran 5-100 % slower exact than padded.
-  // CCMI_CO_PACK=pow2 / exact forces one form where both exist (diagnostics; identical counts).
+  // per step, channels padded to the next power of two KP >= 4, or exact-K packing (ExactK) for
+  // K = 17, 18, where it saves over 40 % of the super-steps.  Measured at C3
+  // (tools/co_only.py, profiles/r03/coassoc_fp4_first.txt): the exact form's expansion costs
+  // more VALU per step, and below K = 17 its register demand spills, so K = 5, 9, 10, 11, 19, 20
+  // ran 5-100 % slower exact than padded; only K = 17, 18 are built exact.
+  // CCMI_CO_PACK=pow2 / exact forces one form for those two (diagnostics; identical counts).
   int kp = K <= 2 ? 2 : 4;
   while (kp < K) kp <<= 1;
-  if (kp != K && K < 32) {
+  if (K == 17 || K == 18) {
     const int hs = 256 / K, se = (Hpad + hs - 1) / hs, sp = Hpad / (256 / kp);
     const char* pk = std::getenv("CCMI_CO_PACK");
     const bool force_pow2 = pk && pk[0] == 'p', force_exact = pk && pk[0] == 'e';
-    if (force_exact || (!force_pow2 && 5 * se <= 3 * sp && K >= 17)) kp = K;
+    if (force_exact || (!force_pow2 && 5 * se <= 3 * sp)) kp = K;
   }
   switch (kp) {
-#define CC_EXACT(k) case k: launch_tiles<k, true>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
-    CC_EXACT(3) CC_EXACT(5) CC_EXACT(6) CC_EXACT(7) CC_EXACT(9) CC_EXACT(10) CC_EXACT(11)
-    CC_EXACT(12) CC_EXACT(13) CC_EXACT(14) CC_EXACT(15) CC_EXACT(17) CC_EXACT(18) CC_EXACT(19)
-    CC_EXACT(20) CC_EXACT(21) CC_EXACT(22) CC_EXACT(23) CC_EXACT(24) CC_EXACT(25) CC_EXACT(26)
-    CC_EXACT(27) CC_EXACT(28) CC_EXACT(29) CC_EXACT(30) CC_EXACT(31)
-    CC_EXACT(4) CC_EXACT(8) CC_EXACT(16) CC_EXACT(32) CC_EXACT(64)
-#undef CC_EXACT
+#define CC_F4(k) case k: launch_tiles<k, true>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
+    CC_F4(4) CC_F4(8) CC_F4(16) CC_F4(17) CC_F4(18) CC_F4(32) CC_F4(64)
+#undef CC_F4
     case 2: launch_tiles<2>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
     default: launch_tiles<128, true>(grid, st, lab, n, ldl, Hpad, tile_begin, nullptr, I_tiles, edges, bin_counts, M_full, bin_table, table_rows); break;
   }

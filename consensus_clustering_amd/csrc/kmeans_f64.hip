@@ -409,6 +409,11 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
             s_flag = (mx == 0.0) ? 0 : ne;
           }
           __syncthreads();
+          // Parity gap (documented): sklearn takes the n_empty farthest rows from
+          // np.argpartition(distances, -n_empty)[:-n_empty-1:-1], whose order among those rows
+          // (and whose tie-break) is introselect's; here empty cluster e takes the e-th farthest
+          // remaining row, lowest index on ties.  The two agree for one empty cluster without
+          // tied distances; with n_empty >= 2 or ties, bit-parity with sklearn is not claimed.
           const int ne = s_flag;
           for (int e = 0; e < ne; ++e) {
             if (tid == 0) {

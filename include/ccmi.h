@@ -116,16 +116,27 @@ int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int K, int64_t
 /* Bin thresholds per co-sampling count i in [0, rows): row i = 21 uint16 T[b] =
  * min{m : bin(f32(m) / f32(i + 1e-6)) >= b} (T[0] = 0, T[20] = 0xFFFF; i + 1 if no m <= i
  * reaches b), so bin = #{b in 1..19 : m >= T[b]} (numpy.histogram semantics, CC.py:338-344).
- * table: device, rows * 21 uint16 in an allocation padded to a multiple of 16 B. */
-int cc_bin_table(int rows, const float* edges, uint16_t* table, void* stream);
+ * table: device, table_bytes >= cc_bin_table_bytes(rows).  After the rows * 21 uint16 (padded
+ * to 16 B) it holds, when rows is small enough for cc_coassoc to stage them on chip, the
+ * threshold pairs T[g] | T[g+1] << 16 (rows * 20 uint32) and the bins themselves for every
+ * (m <= i) pair (one byte at i (i + 1) / 2 + m, padded to 16 B). */
+int cc_bin_table(int rows, const float* edges, uint16_t* table, size_t table_bytes, void* stream);
+
+/* Bytes of the cc_bin_table buffer for `rows` rows (0 when rows is out of range). */
+size_t cc_bin_table_bytes(int rows);
 
 /* Largest table (rows) cc_coassoc can stage on chip. */
 int cc_bin_table_max_rows(void);
 
+/* Largest row count for each staged form: 0 = uint16 thresholds (= cc_bin_table_max_rows),
+ * 1 = threshold pairs, 2 = the bin triangle.  cc_coassoc stages the most compact form that fits. */
+int cc_bin_table_form_rows(int form);
+
 /* Self-test of the division-free binning: for EVERY pair of counts (m <= i < rows), compare
- * the two table forms cc_coassoc uses (threshold table + reciprocal estimate computed per
- * element, and with the staged per-row reciprocal) against the direct numpy-exact bin of
- * f32(m) / f32(i + 1e-6).  mismatches: device [2] uint64, accumulated into. */
+ * the table forms cc_coassoc uses (threshold table + reciprocal estimate computed per
+ * element, and with the staged per-row reciprocal; the threshold pairs and the bin triangle
+ * when the table holds them) against the direct numpy-exact bin of f32(m) / f32(i + 1e-6).
+ * mismatches: device [4] uint64, accumulated into. */
 int cc_bin_selftest(int rows, const float* edges, const uint16_t* table,
                     unsigned long long* mismatches, void* stream);
 

@@ -126,7 +126,7 @@ def test_consensus_matrix_kernel():
     np.testing.assert_array_equal(C, O.consensus_matrix(M.astype(np.uint16), I.astype(np.uint16)))
 
 
-@pytest.mark.parametrize("H,K", [(37, 3), (256, 10), (300, 7), (1000, 20)])
+@pytest.mark.parametrize("H,K", [(37, 3), (256, 10), (300, 7), (1000, 20), (1500, 5)])
 def test_threshold_table_binning_is_exact(H, K):
     """cc_coassoc's division-free binning (cc_bin_table thresholds) gives the same 20 counts as
     the direct numpy-exact bin on every pair (n = 700: tile (0, 1) takes the interior-tile
@@ -164,20 +164,29 @@ def test_bin_table_exhaustive():
     from consensus_clustering_amd import _lib
 
     dev = engine.require_gpu()
-    rows = _lib.load().cc_bin_table_max_rows()
-    tab = engine.bin_table(dev, rows)
-    mism = torch.zeros(2, dtype=torch.int64, device=dev)
-    _lib.call("cc_bin_selftest", rows, engine.edges_device(dev).data_ptr(), tab.data_ptr(),
-              mism.data_ptr(), engine.stream_ptr())
-    torch.cuda.synchronize()
-    assert mism.tolist() == [0, 0], (rows, mism.tolist())
+    lib = _lib.load()
+    assert lib.cc_bin_table_form_rows(0) == lib.cc_bin_table_max_rows()
+    # the largest table of each staged form: uint16 thresholds, threshold pairs, bin triangle
+    for form in (0, 1, 2):
+        rows = lib.cc_bin_table_form_rows(form)
+        tab = engine.bin_table(dev, rows)
+        mism = torch.zeros(4, dtype=torch.int64, device=dev)
+        _lib.call("cc_bin_selftest", rows, engine.edges_device(dev).data_ptr(), tab.data_ptr(),
+                  mism.data_ptr(), engine.stream_ptr())
+        torch.cuda.synchronize()
+        assert mism.tolist() == [0, 0, 0, 0], (form, rows, mism.tolist())
+    assert lib.cc_bin_table_form_rows(2) >= 257 and lib.cc_bin_table_form_rows(1) >= 1025
 
 
+@pytest.mark.parametrize("pack", ["default", "exact", "pow2"])
 @pytest.mark.parametrize("n,H,frac", [(300, 200, 0.7), (260, 1000, 0.8), (129, 37, 1.0)])
-def test_exact_k_packing_every_k(n, H, frac):
-    """Exact-K channel packing (floor(128/K) resamples per super-step, unaligned label starts,
-    a partial last step) against a float one-hot product, for every K of 2..33 with labels
-    drawn uniformly over all K channels."""
+def test_exact_k_packing_every_k(n, H, frac, pack, monkeypatch):
+    """The FP4 one-hot padded to a power of two, its exact-K packing (K = 17, 18: floor(256/K)
+    resamples per super-step, unaligned label starts, a partial last step) and the i8 form of
+    K <= 2, against a float one-hot product, for every K of 2..33 with labels drawn uniformly
+    over all K channels (CCMI_CO_PACK forces a packing where both exist)."""
+    if pack != "default":
+        monkeypatch.setenv("CCMI_CO_PACK", pack)
     dev = engine.require_gpu()
     rng = np.random.default_rng(n * H)
     m = int(frac * n)

@@ -100,7 +100,7 @@ def test_undersized_workspace_is_rejected(precision, dtype):
     L = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
     Ks_np = np.asarray(Ks, dtype=np.int32)
     guard = torch.full((1 << 16,), 0x5A, dtype=torch.uint8, device=dev)
-    for small in (0, 256, 4096):
+    for small in (0, 256, 1024):
         with pytest.raises(_lib.CCMIError, match="workspace too small"):
             _lib.call("cc_kmeans_fit", Xd.data_ptr(), n, d, idx_d.data_ptr(), H, m, 0, H,
                       Ks_np.ctypes.data, len(Ks), 3, 300, 1e-4, ctypes.c_uint32(1), precision,

@@ -233,3 +233,4 @@ def test_f64_labels_match_sklearn_float64(n, d, k_true, Ks, H):
                 assert not np.array_equal(km32.labels_, km.labels_), (K, h, np.mean(km.labels_ == got))
                 ill += 1
     assert exact >= 0.9 * (exact + ill), (exact, ill)
+
