@@ -26,6 +26,8 @@ SIGNATURES = {
     "cc_resample_indices": (_c_int, [_c_u32, _c_int, _c_int, _c_int, _c_int, _vp, _c_int]),
     "cc_resample_device_max_n": (_c_int, []),
     "cc_resample_device": (_c_int, [_c_u32, _c_int, _c_int, _c_int, _c_int, _vp, _vp]),
+    "cc_resample_device_wide": (_c_int, [_c_u32, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_sz, _vp]),
+    "cc_resample_device_wide_workspace_bytes": (_c_sz, [_c_int, _c_int]),
     "cc_random_sample": (_c_int, [_c_u32, _c_i64, _vp]),
     "cc_num_tiles": (_c_i64, [_c_int]),
     "cc_scatter_labels": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),

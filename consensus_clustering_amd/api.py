@@ -7,8 +7,8 @@ when n_iterations < 256 else uint16 (CC.py:107), cij float32 with a unit diagona
 bin_edges float32, hist/cdf float64, pac_area np.float64.
 
 What runs where (``fit``):
-  resampling      numpy-RandomState replay on the device (libccmi cc_resample_device, n <= 65536)
-                  or on host threads (cc_resample_indices)
+  resampling      numpy-RandomState replay on the device (libccmi cc_resample_device /
+                  cc_resample_device_wide) or on host threads (cc_resample_indices)
   clustering      default clusterer (KMeans) -> all (h, K, init) problems in batched
                   gfx950 launches (cc_kmeans_batched); any other plugin clusterer
                   (e.g. GaussianMixture) keeps the reference's host fit_predict per
@@ -107,8 +107,9 @@ class ConsensusClustering:
         # 'fast' = the float32-class f16 hi/lo MFMA engine; 'auto' = f64 for float64 input while
         # the float64 engine's work is small (F64_AUTO_MAX_WORK), else fast with a warning
         self.precision = precision
-        # where the resample indices are drawn: 'device' (cc_resample_device, n <= 65536),
-        # 'host' (native threads, then uploaded), 'auto' = device when n allows; identical draws
+        # where the resample indices are drawn: 'device' (cc_resample_device for n <= 65536,
+        # cc_resample_device_wide above), 'host' (native threads, then uploaded), 'auto' =
+        # device; identical draws
         self.resampling = resampling
         self.timings_ = {}
         self._rehearsal = None  # (rank, world): bench tooling only, see fit()
@@ -187,9 +188,7 @@ class ConsensusClustering:
         h0, h1 = dist.shard(H, rank, W)
         if self.resampling not in ('auto', 'device', 'host'):
             raise ValueError("resampling must be 'auto', 'device' or 'host'")
-        on_dev = self.resampling != 'host' and n <= engine.resample_device_max_n()
-        if self.resampling == 'device' and not on_dev:
-            raise ValueError(f"resampling='device' needs n <= {engine.resample_device_max_n()}")
+        on_dev = self.resampling != 'host'
         self.resampling_ = 'device' if on_dev else 'host'
         idx = None  # host copy, made only when a host consumer needs it (resampling_indices_)
         if on_dev:

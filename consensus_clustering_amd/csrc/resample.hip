@@ -16,9 +16,11 @@
 //     trip per accepted step: read x[i] and x[j], write x[j], store x[j]'s old value to
 //     out[i] when i < m).
 // Resamples are independent, so nothing crosses workgroups; each rank launches only its own
-// h range.  The host replay (host_rng.cpp) stays for n > 65536 (the uint16 array).
+// h range.  Any n: cc_resample_device_wide (below) resolves the shuffle from its swap partners
+// without simulating it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 
@@ -121,9 +123,237 @@ __global__ __launch_bounds__(RS_NT) void resample_kernel(uint32_t seed, int n, i
   if (lane == 0 && m > 0) o[0] = arr[0];
 }
 
+// ---- any n: the shuffle resolved from its swap partners -----------------------------------
+// Step i of the shuffle swaps positions i and J[i] (J[i] = the accepted random_interval(i) draw,
+// J[i] <= i).  Let g(i) be the value at position i just before step i.  Position i was last
+// written before that by the latest earlier step i' > i with J[i'] = i (the smallest such i'),
+// which moved g(i') there; with no such step it still holds i.  So with the steps grouped by
+// partner position (bucket p = {i : J[i] = p}, ascending):
+//   succ(p) = the first step of bucket p greater than p;  g(i) = succ(i) ? g(succ(i)) : i;
+//   out[k] (k >= 1) = the value at J[k] before step k = (next step after k in bucket J[k]) ?
+//                     g(next) : J[k];   out[0] = (first step of bucket 0) ? g(first) : 0.
+// Only the draws are sequential (lane 0 of one wave per resample, no memory round trip per
+// step); buckets are a counting sort, and the g chains are short (mean ~1, max ~20 at n = 200k).
+// Arrays per resample (workspace, uint32 [n] each): J, bucket offsets, cursors, the sorted
+// steps, next-in-bucket, succ.
+constexpr int RSW_ARRAYS = 6;
+
+__global__ __launch_bounds__(RS_NT) void rsw_draw_kernel(uint32_t seed, int n, int h_begin, size_t stride,
+                                                        uint32_t* J) {
+  __shared__ uint32_t mt[MT_N], nw[MT_N];
+  __shared__ __attribute__((aligned(16))) uint32_t draws[MT_N];
+  __shared__ uint32_t stage[MT_N];
+  __shared__ int st_i, st_c;
+  const int lane = threadIdx.x;
+  const int h = h_begin + blockIdx.x;
+  uint32_t* Jh = J + static_cast<size_t>(blockIdx.x) * stride;
+  if (lane == 0) {  // init_genrand(seed + h)
+    uint32_t x = seed + static_cast<uint32_t>(h);
+    mt[0] = x;
+    for (int i = 1; i < MT_N; ++i) {
+      x = 1812433253u * (x ^ (x >> 30)) + static_cast<uint32_t>(i);
+      mt[i] = x;
+    }
+    st_i = n - 1;
+    Jh[0] = 0;
+  }
+  __syncthreads();
+  while (st_i >= 1) {  // wave-uniform
+    mt_block(mt, nw, draws, lane);
+    const int i0 = st_i;
+    if (lane == 0) {
+      int i = i0, c = 0;
+      uint32_t mask = interval_mask(static_cast<uint32_t>(i));
+      for (int p = 0; p < MT_N && i >= 1; p += 4) {
+        const uint4 d4 = *reinterpret_cast<const uint4*>(draws + p);
+        const uint32_t dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (i < 1) break;
+          const uint32_t v = dv[u] & mask;
+          if (v > static_cast<uint32_t>(i)) continue;  // rejected
+          stage[c++] = v;
+          --i;
+          if (static_cast<uint32_t>(i) <= (mask >> 1)) mask >>= 1;
+        }
+      }
+      st_i = i;
+      st_c = c;
+    }
+    __syncthreads();
+    for (int e = lane; e < st_c; e += RS_NT) Jh[i0 - e] = stage[e];  // steps i0, i0 - 1, ...
+    __syncthreads();
+  }
+}
+
+// bucket sizes, then (one workgroup per resample) their exclusive scan -> offsets, cursors zeroed
+__global__ void rsw_count_kernel(int n, int nh, size_t stride, const uint32_t* __restrict__ J, uint32_t* cnt) {
+  const int64_t total = static_cast<int64_t>(nh) * (n - 1);
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t h = e / (n - 1);
+    const int i = static_cast<int>(e - h * (n - 1)) + 1;
+    atomicAdd(&cnt[h * stride + J[h * stride + i]], 1u);
+  }
+}
+
+__global__ __launch_bounds__(256) void rsw_scan_kernel(int n, size_t stride, uint32_t* cnt, uint32_t* cur) {
+  __shared__ uint32_t part[256];
+  uint32_t* c = cnt + static_cast<size_t>(blockIdx.x) * stride;
+  uint32_t* u = cur + static_cast<size_t>(blockIdx.x) * stride;
+  const int t = threadIdx.x;
+  const int per = (n + 255) / 256, b0 = t * per, b1 = min(n, b0 + per);
+  uint32_t s = 0;
+  for (int p = b0; p < b1; ++p) s += c[p];
+  part[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int k = 0; k < 256; ++k) {
+      const uint32_t v = part[k];
+      part[k] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  uint32_t run = part[t];
+  for (int p = b0; p < b1; ++p) {
+    const uint32_t v = c[p];
+    c[p] = run;  // exclusive offset
+    u[p] = 0;
+    run += v;
+  }
+}
+
+__global__ void rsw_scatter_kernel(int n, int nh, size_t stride, const uint32_t* __restrict__ J,
+                                   const uint32_t* __restrict__ off, uint32_t* cur, uint32_t* sorted) {
+  const int64_t total = static_cast<int64_t>(nh) * (n - 1);
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t h = e / (n - 1);
+    const int i = static_cast<int>(e - h * (n - 1)) + 1;
+    const uint32_t p = J[h * stride + i];
+    const uint32_t k = atomicAdd(&cur[h * stride + p], 1u);
+    sorted[h * stride + off[h * stride + p] + k] = static_cast<uint32_t>(i);
+  }
+}
+
+// per bucket p: sort its steps ascending (insertion sort in place: buckets are small), then
+// next-in-bucket for each step and succ(p) (0 = none: every step is >= 1)
+__global__ void rsw_bucket_kernel(int n, int nh, size_t stride, const uint32_t* __restrict__ off,
+                                  const uint32_t* __restrict__ cur, uint32_t* sorted, uint32_t* nxt,
+                                  uint32_t* succ) {
+  const int64_t total = static_cast<int64_t>(nh) * n;
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t h = e / n;
+    const uint32_t p = static_cast<uint32_t>(e - h * n);
+    uint32_t* b = sorted + h * stride + off[h * stride + p];
+    const int len = static_cast<int>(cur[h * stride + p]);
+    for (int a = 1; a < len; ++a) {
+      const uint32_t v = b[a];
+      int q = a - 1;
+      while (q >= 0 && b[q] > v) {
+        b[q + 1] = b[q];
+        --q;
+      }
+      b[q + 1] = v;
+    }
+    uint32_t first = 0;
+    for (int a = 0; a < len; ++a) {
+      nxt[h * stride + b[a]] = (a + 1 < len) ? b[a + 1] : 0u;
+      if (first == 0 && b[a] > p) first = b[a];
+    }
+    succ[h * stride + p] = first;
+  }
+}
+
+__global__ void rsw_out_kernel(int n, int m, int nh, size_t stride, const uint32_t* __restrict__ J,
+                               const uint32_t* __restrict__ off, const uint32_t* __restrict__ cur,
+                               const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ nxt,
+                               const uint32_t* __restrict__ succ, int32_t* __restrict__ out) {
+  const int64_t total = static_cast<int64_t>(nh) * m;
+  for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+       e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t h = e / m;
+    const int k = static_cast<int>(e - h * m);
+    const size_t b = h * stride;
+    uint32_t s, v;
+    if (k == 0) {
+      s = cur[b] ? sorted[b + off[b]] : 0u;
+      v = 0u;
+    } else {
+      s = nxt[b + k];
+      v = J[b + k];
+    }
+    if (s) {  // g(s): follow the chain of first later writers
+      uint32_t x = s;
+      for (uint32_t y = succ[b + x]; y; y = succ[b + x]) x = y;
+      v = x;
+    }
+    out[e] = static_cast<int32_t>(v);
+  }
+}
+
 }  // namespace
 
 extern "C" int cc_resample_device_max_n(void) { return RS_MAXN; }
+
+extern "C" size_t cc_resample_device_wide_workspace_bytes(int n, int nh) {
+  if (n <= 0 || nh <= 0) return 0;
+  return static_cast<size_t>(RSW_ARRAYS) * static_cast<size_t>(nh) * ((static_cast<size_t>(n) + 63) & ~static_cast<size_t>(63)) *
+         sizeof(uint32_t);
+}
+
+extern "C" int cc_resample_device_wide(uint32_t seed, int h_begin, int h_end, int n, int m, int32_t* out,
+                                       void* workspace, size_t ws_bytes, void* stream) {
+  if (n <= 0 || m < 0 || m > n || h_begin < 0 || h_end < h_begin || (h_end > h_begin && m > 0 && !out)) {
+    cc::set_error("cc_resample_device_wide: bad arguments (n >= 1, 0 <= m <= n)");
+    return CC_ERR_ARG;
+  }
+  if (static_cast<uint64_t>(seed) + static_cast<uint64_t>(h_end) > 0xffffffffull + 1) {
+    cc::set_error("cc_resample_device_wide: seed + h exceeds 2**32 - 1 (numpy raises ValueError)");
+    return CC_ERR_ARG;
+  }
+  const int H = h_end - h_begin;
+  if (H == 0 || m == 0) return CC_OK;
+  const size_t per = cc_resample_device_wide_workspace_bytes(n, 1);
+  if (!workspace || ws_bytes < per) {
+    cc::set_error("cc_resample_device_wide: workspace too small (cc_resample_device_wide_workspace_bytes(n, 1) at least)");
+    return CC_ERR_ARG;
+  }
+  const int batch = static_cast<int>(std::min<size_t>(static_cast<size_t>(H), ws_bytes / per));
+  const size_t stride = (static_cast<size_t>(n) + 63) & ~static_cast<size_t>(63);
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  for (int hb = 0; hb < H; hb += batch) {
+    const int nh = std::min(batch, H - hb);
+    uint32_t* base = static_cast<uint32_t*>(workspace);
+    const size_t A = static_cast<size_t>(nh) * stride;
+    uint32_t *J = base, *off = base + A, *cur = base + 2 * A, *sorted = base + 3 * A, *nxt = base + 4 * A,
+             *succ = base + 5 * A;
+    if (hipMemsetAsync(off, 0, A * sizeof(uint32_t), st) != hipSuccess) {
+      cc::set_error("cc_resample_device_wide: memset failed");
+      return CC_ERR_HIP;
+    }
+    hipLaunchKernelGGL(rsw_draw_kernel, dim3(nh), dim3(RS_NT), 0, st, seed, n, h_begin + hb, stride, J);
+    const int64_t work = static_cast<int64_t>(nh) * n;
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>((work + 255) / 256, 65536));
+    if (n > 1) hipLaunchKernelGGL(rsw_count_kernel, dim3(g), dim3(256), 0, st, n, nh, stride, J, off);
+    hipLaunchKernelGGL(rsw_scan_kernel, dim3(nh), dim3(256), 0, st, n, stride, off, cur);
+    if (n > 1) hipLaunchKernelGGL(rsw_scatter_kernel, dim3(g), dim3(256), 0, st, n, nh, stride, J, off, cur, sorted);
+    hipLaunchKernelGGL(rsw_bucket_kernel, dim3(g), dim3(256), 0, st, n, nh, stride, off, cur, sorted, nxt, succ);
+    const int64_t owork = static_cast<int64_t>(nh) * m;
+    const unsigned go = static_cast<unsigned>(std::min<int64_t>((owork + 255) / 256, 65536));
+    hipLaunchKernelGGL(rsw_out_kernel, dim3(go), dim3(256), 0, st, n, m, nh, stride, J, off, cur, sorted, nxt, succ,
+                       out + static_cast<size_t>(hb) * m);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      cc::set_error(std::string("cc_resample_device_wide: ") + hipGetErrorString(e));
+      return CC_ERR_HIP;
+    }
+  }
+  return CC_OK;
+}
 
 extern "C" int cc_resample_device(uint32_t seed, int h_begin, int h_end, int n, int m, int32_t* out,
                                   void* stream) {

@@ -86,11 +86,17 @@ def resample_indices(seed: int, n: int, m: int, h_begin: int, h_end: int, n_thre
     return out
 
 
+# workspace cap of the swap-partner resampling (resamples run in batches that fit)
+RESAMPLE_WIDE_WS = 1 << 30
+
+
 def resample_indices_device(seed: int, n: int, m: int, h_begin: int, h_end: int, device,
-                            out: torch.Tensor | None = None) -> torch.Tensor:
-    """int32 [h_end-h_begin, m] on the device: the same draws as resample_indices, generated by
-    cc_resample_device (one workgroup per resample; n <= 65536).  `out`: a contiguous int32
-    device tensor of that shape to fill (e.g. a row slice of the full [H, m] matrix)."""
+                            out: torch.Tensor | None = None, method: str = "auto") -> torch.Tensor:
+    """int32 [h_end-h_begin, m] on the device: the same draws as resample_indices.
+    method 'swap': cc_resample_device (the shuffle simulated in LDS; n <= 65536); 'wide':
+    cc_resample_device_wide (any n, resolved from the swap partners); 'auto': wide when
+    n > 65536 else swap.  `out`: a contiguous int32 device tensor of that shape to fill (e.g. a
+    row slice of the full [H, m] matrix)."""
     if seed is None:
         raise TypeError("unsupported operand type(s) for +: 'NoneType' and 'int'")
     seed = int(seed)
@@ -101,12 +107,27 @@ def resample_indices_device(seed: int, n: int, m: int, h_begin: int, h_end: int,
     elif (tuple(out.shape) != (h_end - h_begin, m) or out.dtype != torch.int32 or not out.is_contiguous()
           or not out.is_cuda):
         raise ValueError("out must be a contiguous int32 device tensor of shape [h_end - h_begin, m]")
-    _lib.call("cc_resample_device", ctypes.c_uint32(seed), h_begin, h_end, n, m,
-              out.data_ptr() if out.numel() else None, stream_ptr(device))
+    if method == "auto":
+        method = "wide" if n > resample_device_max_n() else "swap"
+    if method == "swap":
+        _lib.call("cc_resample_device", ctypes.c_uint32(seed), h_begin, h_end, n, m,
+                  out.data_ptr() if out.numel() else None, stream_ptr(device))
+    elif method == "wide":
+        lib = _lib.load()
+        nh = max(h_end - h_begin, 1)
+        per = int(lib.cc_resample_device_wide_workspace_bytes(n, 1))
+        nb = max(1, min(nh, RESAMPLE_WIDE_WS // max(per, 1)))
+        ws = torch.empty(per * nb, dtype=torch.uint8, device=device)
+        _lib.call("cc_resample_device_wide", ctypes.c_uint32(seed), h_begin, h_end, n, m,
+                  out.data_ptr() if out.numel() else None, ws.data_ptr(), ws.numel(),
+                  stream_ptr(device))
+    else:
+        raise ValueError("method must be 'auto', 'swap' or 'wide'")
     return out
 
 
 def resample_device_max_n() -> int:
+    """Largest n of the LDS shuffle (cc_resample_device); the wide form has no limit."""
     return int(_lib.load().cc_resample_device_max_n())
 
 

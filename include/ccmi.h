@@ -13,6 +13,7 @@
  *
  *   cc_resample_indices   CC.py:216-241  _get_subsampling_indices (numpy RandomState replay)
  *   cc_resample_device    the same on the device (n <= 65536), straight into HBM
+ *   cc_resample_device_wide  the same for any n, without simulating the shuffle
  *   cc_scatter_labels     CC.py:260-262, :284-285  indicator / one-hot row placement
  *   cc_copy_label_columns CC.py:185-195 (the parallel paths' shared M) -> multi-GPU label exchange
  *   cc_cosample           CC.py:264  I = S^T S            (int8 MFMA, upper-triangle tiles)
@@ -78,6 +79,16 @@ int64_t cc_num_tiles(int n);
 int cc_resample_device_max_n(void);
 int cc_resample_device(uint32_t seed, int h_begin, int h_end, int n, int m, int32_t* out,
                        void* stream);
+
+/* The same draws for any n (no 65536 limit): RandomState(seed + h).permutation(n)[:m] resolved
+ * from the shuffle's swap partners (the draws on one lane per resample, a counting sort of the
+ * steps by partner, then each output value as the end of a short chain of later writers), so no
+ * step of the shuffle is simulated.  workspace: device, ws_bytes >= the bytes for one resample;
+ * resamples run in batches that fit (cc_resample_device_wide_workspace_bytes(n, nh) for nh at
+ * once).  Asynchronous on `stream`; out as cc_resample_device. */
+int cc_resample_device_wide(uint32_t seed, int h_begin, int h_end, int n, int m, int32_t* out,
+                            void* workspace, size_t ws_bytes, void* stream);
+size_t cc_resample_device_wide_workspace_bytes(int n, int nh);
 
 /* labels_nh[idx[h][r] * ldl + h] = labels_hm ? labels_hm[h*m + r] : 0 for h < H, r < m.
  * labels_nh must be pre-filled with 0xFF (= not sampled).  (CC.py:260-262, :284-285) */

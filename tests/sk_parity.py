@@ -3,12 +3,15 @@ KMeans called as CC.py:205-214 / :282 call it.  Not a test module."""
 import numpy as np
 
 
-def sklearn_parity(X, labels, idx, Ks, seed, resamples, skip=0, threads=16, n_init=3):
+def sklearn_parity(X, labels, idx, Ks, seed, resamples, skip=0, threads=16, n_init=3, max_unexplained=0):
     """Labels of resamples skip .. skip + resamples - 1 of every K against sklearn's float32
-    KMeans on the same rows.  A disagreement is allowed only where sklearn's own float32 and
-    float64 fits of those rows disagree (the partition hinges on rounding, the accuracy class
-    the f16 hi/lo MFMA engine shares with sklearn's float32 sgemm).  Prints and returns
-    (identical, explained, total); asserts that no disagreement is unexplained.
+    KMeans on the same rows.  A disagreement is allowed only where the partition hinges on
+    rounding, shown by sklearn itself: its float32 and float64 fits of those rows disagree, or
+    its float32 fit changes when every value is moved by a relative 2^-22 (the operand precision
+    of the f16 hi/lo MFMA engine, which shares sklearn float32's accuracy class, not its
+    rounding).  Prints and returns (identical, explained, total); asserts
+    that at most `max_unexplained` disagreements are unexplained (0 unless a caller documents
+    a known gap).
 
     labels: the fit's device label matrix [nK, n, Hpad] (uint8) or a host array
     [nK, H, m] of labels in resample order."""
@@ -31,10 +34,21 @@ def sklearn_parity(X, labels, idx, Ks, seed, resamples, skip=0, threads=16, n_in
                     rows.astype(np.float64))
                 if not np.array_equal(ref32, ref64):
                     explained += 1
+                    continue
+                # sklearn's own float32 fit of the same rows, each value moved by the engine's
+                # operand precision (x = xh + xl in f16: 22 significant bits, a relative 2^-22, two
+                # float32 ulps) in a random direction: if that changes the partition, it hinges on
+                # rounding at the engine's accuracy class
+                rng = np.random.default_rng(1000 * K + h)
+                sign = np.where(rng.random(rows.shape) < 0.5, 1.0, -1.0)
+                nudged = (rows.astype(np.float64) * (1.0 + sign * 2.0 ** -22)).astype(np.float32)
+                refn = KMeans(n_clusters=K, random_state=seed, n_init=n_init).fit_predict(nudged)
+                if not np.array_equal(ref32, refn):
+                    explained += 1
                 else:
                     unexplained.append((K, h, float(np.mean(ref32 == got))))
     total = len(Ks) * resamples
-    print(f"sklearn parity: {same}/{total} identical, {explained} differ where sklearn f32 != f64, "
-          f"{len(unexplained)} unexplained {unexplained}")
-    assert not unexplained, unexplained
+    print(f"sklearn parity: {same}/{total} identical, {explained} differ where sklearn's own float32 "
+          f"fit is rounding-sensitive, {len(unexplained)} unexplained {unexplained}")
+    assert len(unexplained) <= max_unexplained, unexplained
     return same, explained, total

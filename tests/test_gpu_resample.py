@@ -1,4 +1,5 @@
-"""Resampling on the device (cc_resample_device) against numpy and the host replay.
+"""Resampling on the device (cc_resample_device, and cc_resample_device_wide for any n) against
+numpy and the host replay.
 
 Reference: consensus_clustering_parallelised.py:231-239 (`_get_subsampling_indices`): resample h
 is RandomState(random_state + h).choice(n, m, replace=False) == permutation(n)[:m].  The device
@@ -39,9 +40,10 @@ def test_c3_shape_all_resamples_match_host_and_numpy():
     (10_000, 8_000, 490, 500, 0),       # C2 shape, tail of the range
     (4_097, 17, 0, 2, 2**32 - 2),       # seed + h up to 2**32 - 1
 ])
-def test_edge_shapes_match_numpy(n, m, h0, h1, seed):
+@pytest.mark.parametrize("method", ["swap", "wide"])
+def test_edge_shapes_match_numpy(n, m, h0, h1, seed, method):
     dev = engine.require_gpu()
-    got = engine.resample_indices_device(seed, n, m, h0, h1, dev).cpu().numpy()
+    got = engine.resample_indices_device(seed, n, m, h0, h1, dev, method=method).cpu().numpy()
     assert got.shape == (h1 - h0, m)
     for k, h in enumerate(range(h0, h1)):
         np.testing.assert_array_equal(got[k], _numpy(seed, n, m, h))
@@ -52,10 +54,29 @@ def test_empty_and_rejected_arguments():
     assert engine.resample_indices_device(0, 100, 0, 0, 4, dev).shape == (4, 0)
     assert engine.resample_indices_device(0, 100, 80, 3, 3, dev).shape == (0, 80)
     with pytest.raises(_lib.CCMIError):
-        engine.resample_indices_device(0, engine.resample_device_max_n() + 1, 10, 0, 1, dev)
+        engine.resample_indices_device(0, engine.resample_device_max_n() + 1, 10, 0, 1, dev, method="swap")
+    assert engine.resample_indices_device(0, 100, 0, 0, 4, dev, method="wide").shape == (4, 0)
     with pytest.raises(ValueError):
         engine.resample_indices_device(2**32 - 1, 10, 5, 0, 2, dev)
     torch.cuda.synchronize()
+
+
+def test_c5_shape_wide_matches_host_and_numpy():
+    """C5: n = 200 000 > 65 536 (beyond the LDS shuffle), m = 160 000, H = 256: every resample
+    of cc_resample_device_wide against the host replay, three against numpy itself; the
+    workspace cap forces several resample batches."""
+    dev = engine.require_gpu()
+    n, m, H, seed = 200_000, 160_000, 256, 0
+    cap = engine.RESAMPLE_WIDE_WS
+    engine.RESAMPLE_WIDE_WS = 100 << 20  # 21 resamples per batch
+    try:
+        got = engine.resample_indices_device(seed, n, m, 0, H, dev).cpu().numpy()
+    finally:
+        engine.RESAMPLE_WIDE_WS = cap
+    ref = engine.resample_indices(seed, n, m, 0, H)
+    np.testing.assert_array_equal(got, ref)
+    for h in (0, 1, H - 1):
+        np.testing.assert_array_equal(got[h], _numpy(seed, n, m, h))
 
 
 def test_fit_device_and_host_resampling_identical():

@@ -1,4 +1,5 @@
-"""Resampling time at a config's shape: cc_resample_device (HIP events) against the host replay
+"""Resampling time at a config's shape: the device forms (HIP events; method swap =
+cc_resample_device when n <= 65536, wide = cc_resample_device_wide) against the host replay
 cc_resample_indices plus its upload (wall clock).
 
     python tools/rs_time.py [config] [reps]
@@ -20,20 +21,25 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 dev = engine.require_gpu()
 n, H = cfg["n"], cfg["H"]
 m = int(cfg["frac"] * n)
-dv, hv = [], []
+methods = ["wide"] + (["swap"] if n <= engine.resample_device_max_n() else [])
+dv, hv = {k: [] for k in methods}, []
 for r in range(reps + 1):
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    d = engine.resample_indices_device(0, n, m, 0, H, dev)
-    b.record()
-    torch.cuda.synchronize()
+    outs = {}
+    for meth in methods:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        outs[meth] = engine.resample_indices_device(0, n, m, 0, H, dev, method=meth)
+        b.record()
+        torch.cuda.synchronize()
+        if r:
+            dv[meth].append(a.elapsed_time(b))
     t0 = time.perf_counter()
     h = torch.from_numpy(engine.resample_indices(0, n, m, 0, H)).to(dev)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if r:
-        dv.append(a.elapsed_time(b))
         hv.append((t1 - t0) * 1e3)
-assert torch.equal(d, h)
-print(f"n={n} m={m} H={H}: device {np.round(dv, 2).tolist()} ms, host replay + upload {np.round(hv, 2).tolist()} ms "
-      f"(host threads {os.cpu_count()})", flush=True)
+    for meth in methods:
+        assert torch.equal(outs[meth], h), meth
+print(f"n={n} m={m} H={H}: " + ", ".join(f"device {k} {np.round(v, 2).tolist()} ms" for k, v in dv.items())
+      + f", host replay + upload {np.round(hv, 2).tolist()} ms (host threads {os.cpu_count()})", flush=True)
