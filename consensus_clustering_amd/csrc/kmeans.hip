@@ -146,9 +146,10 @@ struct KArgs {
   unsigned long long* stats;
   unsigned* counter;
   uint8_t* ws;
-  size_t ws_per_wg, off_cen, off_cenn, off_cpos, off_dbuf, off_rdist;
+  size_t ws_per_wg, off_cen, off_cenn, off_cpos, off_dbuf, off_rdist, off_s64, off_c64, off_list;
   int Pws, Kws, Tws, seedmax;
-  int lsm;  // glab row stride (m rounded up to 64)
+  int lsm;   // glab row stride (m rounded up to 64)
+  int lseg;  // change-list entries per problem and wave segment
 };
 
 struct State {
@@ -162,6 +163,7 @@ struct State {
   unsigned char need_sel[PMAX], to_run[PMAX], sbest[PMAX], lcur[PMAX];
   short cenoff[PMAX], pitem[PMAX];
   int iter[PMAX], amax[PMAX], nempty[PMAX];
+  int pchg[PMAX];  // labels changed in the problem's last Lloyd E-step (m before the first)
   float pot32[PMAX], inert[PMAX];
   int cand[PMAX][TMAX];
   // sweep
@@ -174,6 +176,8 @@ struct State {
   short ioff[IMAX], incol[IMAX];
   double iinert[IMAX];
   unsigned ichanged[IMAX];
+  unsigned char isparse[IMAX];  // RUN item whose sums follow its change list (no M-step MFMAs)
+  unsigned lcnt[IMAX][NW];      // changed labels of a sparse item per wave segment of its rows
   short sitem[CW], scl[CW];
   int srow[CW];  // >= 0: X row (seeding candidate); < 0: -(centre row) - 1
   alignas(16) float cnorm[CW];
@@ -184,7 +188,7 @@ struct State {
   int red_i[NW];
   int map[KMAX + 1];
   int flag;
-  unsigned long long n_lloyd, n_seed, n_mrows, n_reloc, n_sweeps, n_ctiles;
+  unsigned long long n_lloyd, n_seed, n_mrows, n_reloc, n_sweeps, n_ctiles, n_sparse, n_changes;
 };
 
 template <int DP>
@@ -464,6 +468,140 @@ __device__ void relocate(const KArgs& a, const int32_t* idx, int p, int off, con
       S.n_reloc += 1;
     }
     __syncthreads();
+  }
+}
+
+// Wave w's part of the post-sweep label compare of a sparse item: rows [w * seg, (w + 1) * seg)
+// (seg = m / 8 rounded up to 16), 16 rows per lane and load; each changed row is appended to the
+// wave's segment of the item's change list as (row, old | new << 8), in row order (wave prefix
+// sum of the lanes' counts).  Returns the segment's count (it may exceed the capacity `cap`:
+// then only the count is meaningful).
+__device__ unsigned list_changes(const uint8_t* cur, const uint8_t* old, int m, int w, int lane, uint2* seg,
+                                 unsigned cap) {
+  const int rs = (((m + NW - 1) / NW) + 15) & ~15;
+  const int r0 = w * rs, r1 = min(m, r0 + rs);
+  unsigned n = 0;
+  for (int b = r0; b < r1; b += 16 * 64) {  // wave-uniform
+    const int r = b + 16 * lane;
+    unsigned msk = 0;
+    uint4 x = make_uint4(0, 0, 0, 0), y = x;
+    if (r < r1) {  // r1 - r is a multiple of 16 except at m (rows past m hold 0xFF in both buffers)
+      x = *reinterpret_cast<const uint4*>(cur + r);
+      y = *reinterpret_cast<const uint4*>(old + r);
+      const unsigned xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned dq = xs[q] ^ ys[q];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) msk |= ((dq >> (8 * k)) & 0xFFu) ? (1u << (4 * q + k)) : 0u;
+      }
+    }
+    const unsigned c = __popc(msk);
+    unsigned pre = c;  // inclusive wave scan of the counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned t = __shfl_up(pre, o);
+      if (lane >= o) pre += t;
+    }
+    unsigned pos = n + pre - c;
+    const unsigned xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+    while (msk) {
+      const int k = __builtin_ctz(msk);
+      msk &= msk - 1;
+      const unsigned nv = (xs[k >> 2] >> (8 * (k & 3))) & 0xFFu, ov = (ys[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+      if (pos < cap) seg[pos] = make_uint2(static_cast<unsigned>(r + k), ov | (nv << 8));
+      ++pos;
+    }
+    n += __shfl(pre, 63);
+  }
+  return n;
+}
+
+// Sums and counts of a sparse RUN item from its change list, one wave (lane = DP / 64 dims): the
+// entries (segments in wave order, each in row order) add their f32 row to the new cluster's
+// row of acc and subtract it from the old one's (f32; acc = the item's own K rows of Sm, which
+// the M-step leaves alone for a sparse item), 16 row loads in flight; counts by LDS atomics into
+// cnt.  With `full` (a segment overflowed) every row's label `lab` counts as an entry that moved
+// in from nowhere.  The order of additions depends only on the list, so the results do not
+// depend on how the sweeps were packed.  The caller adds acc / cnt into the running sums.
+template <int DP>
+__device__ void apply_changes(const KArgs& a, const int32_t* idx, const uint2* lst, const unsigned* nseg,
+                              bool full, const uint8_t* lab, float* acc, unsigned* cnt, int K, int lane) {
+  constexpr int DL = DP >= 64 ? DP / 64 : 1;  // dims per lane (lanes >= 32 idle at DP = 32)
+  const bool dok = lane * DL < DP;
+  const int d0 = dok ? lane * DL : 0;
+  for (int e = lane; e < K * DP; e += 64) acc[e] = 0.f;
+  if (lane < K) cnt[lane] = 0u;
+  for (int sg = 0; sg < (full ? 1 : NW); ++sg) {
+    const int n = full ? a.m : static_cast<int>(nseg[sg]);
+    const uint2* ls = lst + static_cast<size_t>(sg) * a.lseg;
+    for (int e0 = 0; e0 < n; e0 += 64) {
+      const int e = e0 + lane;
+      unsigned xr = 0, o = 0xFFu, nw = 0xFFu;
+      if (e < n) {
+        unsigned r;
+        if (full) {
+          r = static_cast<unsigned>(e);
+          nw = lab[e];
+        } else {
+          const uint2 v = ls[e];
+          r = v.x;
+          o = v.y & 0xFFu;
+          nw = (v.y >> 8) & 0xFFu;
+        }
+        xr = static_cast<unsigned>(idx[r]);
+        if (nw < 0xFFu) __hip_atomic_fetch_add(&cnt[nw], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (o < 0xFFu) __hip_atomic_fetch_add(&cnt[o], ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      const int ne = min(64, n - e0);
+      constexpr int B = 16;
+      for (int j0 = 0; j0 < ne; j0 += B) {  // wave-uniform
+        float v[B][DL];
+        unsigned jn[B], jo[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) {  // the batch's row loads in flight together
+          const int jj = min(j0 + j, ne - 1);
+          const unsigned row = __builtin_amdgcn_readlane(xr, jj);
+          jn[j] = (j0 + j < ne) ? __builtin_amdgcn_readlane(nw, jj) : 0xFFu;
+          jo[j] = (j0 + j < ne) ? __builtin_amdgcn_readlane(o, jj) : 0xFFu;
+          const float* xp = a.X + static_cast<size_t>(row) * DP + d0;
+          if constexpr (DL == 2) {
+            const float2 q = *reinterpret_cast<const float2*>(xp);
+            v[j][0] = q.x;
+            v[j][DL - 1] = q.y;
+          } else {
+            v[j][0] = *xp;
+          }
+        }
+        if (dok) {
+#pragma unroll
+          for (int j = 0; j < B; ++j) {  // in list order (one wave's LDS accesses stay ordered)
+            if (jn[j] < 0xFFu) {
+              float* q = acc + jn[j] * DP + d0;
+              if constexpr (DL == 2) {
+                float2 t = *reinterpret_cast<float2*>(q);
+                t.x += v[j][0];
+                t.y += v[j][DL - 1];
+                *reinterpret_cast<float2*>(q) = t;
+              } else {
+                *q += v[j][0];
+              }
+            }
+            if (jo[j] < 0xFFu) {
+              float* q = acc + jo[j] * DP + d0;
+              if constexpr (DL == 2) {
+                float2 t = *reinterpret_cast<float2*>(q);
+                t.x -= v[j][0];
+                t.y -= v[j][DL - 1];
+                *reinterpret_cast<float2*>(q) = t;
+              } else {
+                *q -= v[j][0];
+              }
+            }
+          }
+        }
+      }
+    }
   }
 }
 
@@ -1015,6 +1153,10 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_
     }
     S.pitem[p] = static_cast<short>(ni);
     const int kind = (st == ST_RUN) ? IK_RUN : IK_FINAL;
+    // sparse: the sums follow the labels that changed (few moved in the last E-step; no M-step
+    // MFMAs); dense: the M-step recomputes them (the first iteration, after a burst of changes)
+    const bool sparse = st == ST_RUN && S.pchg[p] <= a.m / 8;
+    S.isparse[ni] = static_cast<unsigned char>(sparse);
     S.ikind[ni] = static_cast<unsigned char>(kind);
     S.iprob[ni] = static_cast<unsigned char>(p);
     S.ioff[ni] = static_cast<short>(off);
@@ -1025,7 +1167,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_
     S.iw1[ni] = 0;
     for (int c = 0; c < K4; ++c) {
       S.sitem[off + c] = static_cast<short>(c < K ? ni : -1);
-      S.scl[off + c] = static_cast<short>((st == ST_RUN && c < K) ? c : -1);
+      S.scl[off + c] = static_cast<short>((st == ST_RUN && !sparse && c < K) ? c : -1);  // M-step slots
       S.srow[off + c] = (c < K) ? -(S.cenoff[p] + c) - 1 : INT_MIN;
     }
     ++ni;
@@ -1034,6 +1176,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_
     last = p;
     nlloyd += static_cast<unsigned long long>(K) * a.m;
     if (st == ST_RUN) nm += a.m;
+    S.n_sparse += sparse;
   }
   S.rr = (first_skip >= 0) ? first_skip : (last >= 0 ? (last + 1) % P : S.rr);
   // deal the E-steps to the waves (LPT: heaviest first onto the least loaded wave).  Distance
@@ -1104,14 +1247,17 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m = a.m, T = a.T;
   uint8_t* wsb = a.ws + static_cast<size_t>(blockIdx.x) * a.ws_per_wg;
-  uint8_t* glab = wsb;                                                  // [Pws][m]
+  uint8_t* glab = wsb;                                                  // [2 Pws][lsm]
+  double* s64 = reinterpret_cast<double*>(wsb + a.off_s64);             // [Cws][DP] running sums
+  int* c64 = reinterpret_cast<int*>(wsb + a.off_c64);                   // [Cws] running counts
+  uint2* clist = reinterpret_cast<uint2*>(wsb + a.off_list);            // [Pws][NW][lseg] changes
   float* cen = reinterpret_cast<float*>(wsb + a.off_cen);               // [Cws][DP]
   float* cenn = reinterpret_cast<float*>(wsb + a.off_cenn);             // [Cws]
   int32_t* cpos = reinterpret_cast<int32_t*>(wsb + a.off_cpos);         // [Pws][Kws]
   float* dbuf = reinterpret_cast<float*>(wsb + a.off_dbuf);             // [seedmax][Tws+1][m]
   float* rdist = reinterpret_cast<float*>(wsb + a.off_rdist);           // [m]
   const int T1 = a.Tws + 1;
-  if (tid == 0) S.n_lloyd = S.n_seed = S.n_mrows = S.n_reloc = S.n_sweeps = S.n_ctiles = 0;
+  if (tid == 0) S.n_lloyd = S.n_seed = S.n_mrows = S.n_reloc = S.n_sweeps = S.n_ctiles = S.n_sparse = S.n_changes = 0;
 
   for (;;) {
     __syncthreads();
@@ -1136,6 +1282,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         S.ntr[p] = static_cast<unsigned char>(gd[4 + 4 * p]);
         S.st[p] = ST_WAIT;
         S.iter[p] = 0;
+        S.pchg[p] = a.m;
         S.lcur[p] = 0;
         S.cenoff[p] = static_cast<short>(o);
         o += S.K[p];
@@ -1415,6 +1562,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
             S.seedfree |= 1u << S.sslot[p];
             S.st[p] = ST_RUN;
             S.iter[p] = 0;
+            S.pchg[p] = a.m;
           }
       }
       // candidate selection: one wave per problem
@@ -1442,24 +1590,81 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       // one, 16 B per thread and load, every item in one pass (flags set by any thread that sees
       // a difference: one barrier for all items instead of one per item); then this sweep's
       // buffer becomes the current one
-      if (tid < nitems) S.ichanged[tid] = 0;
-      __syncthreads();
+      // ---- labels changed? (RUN items): compare this sweep's label buffer with the previous
+      // one, each wave over its eighth of the rows; the changed rows of a sparse item go to its
+      // change list (a dense item's are only counted); then this sweep's buffer becomes the
+      // current one
       for (int it = 0; it < nitems; ++it) {
         if (S.ikind[it] != IK_RUN) continue;
         const int p = S.iprob[it];
-        const uint4* cur = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + 1 - S.lcur[p]) * a.lsm);
-        const uint4* old = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm);
-        bool diff = false;
-        for (int e = tid; e < (m + 15) / 16; e += NT) {
-          const uint4 x = cur[e], y = old[e];
-          diff |= (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
+        const uint8_t* cur = glab + static_cast<size_t>(2 * p + 1 - S.lcur[p]) * a.lsm;
+        const uint8_t* old = glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm;
+        const unsigned nc = list_changes(cur, old, m, wave, lane, clist + (static_cast<size_t>(p) * NW + wave) * a.lseg,
+                                         S.isparse[it] ? static_cast<unsigned>(a.lseg) : 0u);
+        if (lane == 0) S.lcnt[it][wave] = nc;
+      }
+      __syncthreads();
+      if (tid < nitems) {
+        const int it = tid;
+        S.ichanged[it] = 0;
+        if (S.ikind[it] == IK_RUN) {
+          unsigned tot = 0;
+          bool over = false;
+          for (int w = 0; w < NW; ++w) {
+            tot += S.lcnt[it][w];
+            over |= S.lcnt[it][w] > static_cast<unsigned>(a.lseg);
+          }
+          S.pchg[S.iprob[it]] = static_cast<int>(tot);
+          S.ichanged[it] = (tot != 0) | ((S.isparse[it] && over) ? 2u : 0u);  // 2: rebuild the sums
         }
-        if (diff) S.ichanged[it] = 1;
       }
       __syncthreads();
       if (tid == 0)
         for (int it = 0; it < nitems; ++it)
-          if (S.ikind[it] >= IK_RUN) S.lcur[S.iprob[it]] = static_cast<unsigned char>(1 - S.lcur[S.iprob[it]]);
+          if (S.ikind[it] >= IK_RUN) {
+            S.lcur[S.iprob[it]] = static_cast<unsigned char>(1 - S.lcur[S.iprob[it]]);
+            if (S.ikind[it] == IK_RUN) S.n_changes += static_cast<unsigned>(S.pchg[S.iprob[it]]);
+          }
+      __syncthreads();
+
+      // ---- running sums: dense items take the M-step's sums; sparse items add their change
+      // lists (one wave per item) into the f64 sums, which then feed the centre update below
+      for (int e = tid; e < ncols * DP; e += NT) {
+        const int sl = e / DP, d = e - sl * DP;
+        const int it = S.sitem[sl];
+        if (it < 0 || S.ikind[it] != IK_RUN || S.isparse[it] || sl - S.ioff[it] >= S.K[S.iprob[it]]) continue;
+        const int row = S.cenoff[S.iprob[it]] + (sl - S.ioff[it]);
+        s64[static_cast<size_t>(row) * DP + d] = static_cast<double>(Sm[e]);
+        if (d == 0) c64[row] = static_cast<int>(S.cnt[sl]);
+      }
+      {
+        int j = 0;
+        for (int it = 0; it < nitems; ++it) {
+          if (S.ikind[it] != IK_RUN || !S.isparse[it]) continue;
+          if ((j++ % NW) != wave) continue;
+          const int p = S.iprob[it], off = S.ioff[it];
+          apply_changes<DP>(a, idx, clist + static_cast<size_t>(p) * NW * a.lseg, S.lcnt[it], (S.ichanged[it] & 2u) != 0,
+                            glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm, Sm + static_cast<size_t>(off) * DP,
+                            S.cnt + off, S.K[p], lane);
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < ncols * DP; e += NT) {  // sparse items: f64 sums += the f32 deltas
+        const int sl = e / DP, d = e - sl * DP;
+        const int it = S.sitem[sl];
+        if (it < 0 || S.ikind[it] != IK_RUN || !S.isparse[it] || sl - S.ioff[it] >= S.K[S.iprob[it]]) continue;
+        const int row = S.cenoff[S.iprob[it]] + (sl - S.ioff[it]);
+        const bool full = (S.ichanged[it] & 2u) != 0;
+        double* sp = s64 + static_cast<size_t>(row) * DP + d;
+        const double t = (full ? 0.0 : *sp) + static_cast<double>(Sm[e]);
+        *sp = t;
+        Sm[e] = static_cast<float>(t);
+        if (d == 0) {
+          const int c = (full ? 0 : c64[row]) + static_cast<int>(S.cnt[sl]);
+          c64[row] = c;
+          S.cnt[sl] = static_cast<unsigned>(c);
+        }
+      }
       __syncthreads();
 
       // ---- Lloyd M-step completion (RUN items) ------------------------------------
@@ -1632,6 +1837,8 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     atomicAdd(&a.stats[3], S.n_reloc);
     atomicAdd(&a.stats[4], S.n_sweeps);
     atomicAdd(&a.stats[5], S.n_ctiles);
+    atomicAdd(&a.stats[6], S.n_sparse);
+    atomicAdd(&a.stats[7], S.n_changes);
   }
 }
 
@@ -1651,9 +1858,15 @@ __global__ void split_kernel(const float* X, long long total, int dpad, float sc
 int local_trials(int K) { return 2 + static_cast<int>(std::log(static_cast<double>(K))); }
 
 struct WsLayout {
-  int Pws = 0, Cws = 0, Kws = 0, Tws = 0;
-  size_t off_cen = 0, off_cenn = 0, off_cpos = 0, off_dbuf = 0, off_rdist = 0, per_wg = 0;
+  int Pws = 0, Cws = 0, Kws = 0, Tws = 0, lseg = 0;
+  size_t off_cen = 0, off_cenn = 0, off_cpos = 0, off_dbuf = 0, off_rdist = 0, off_s64 = 0, off_c64 = 0,
+         off_list = 0, per_wg = 0;
 };
+
+// Change-list entries per problem and wave segment (a segment covers m / 8 rows): a sparse
+// iteration expects at most m / 8 changed labels (the scheduler's threshold); a segment that
+// overflows makes the post-sweep phase rebuild the sums from every label instead.
+int list_seg(int m) { return std::max(16, ((m / 16) + 15) & ~15); }
 
 constexpr size_t WS_HEADER = 256;  // the work counter
 
@@ -1676,7 +1889,11 @@ WsLayout ws_layout(int m, int dpad, const int32_t* units, int nU, int seedmax) {
   L.off_cpos = L.off_cenn + al(static_cast<size_t>(L.Cws) * sizeof(float));
   L.off_dbuf = L.off_cpos + al(static_cast<size_t>(L.Pws) * L.Kws * sizeof(int32_t));
   L.off_rdist = L.off_dbuf + al(static_cast<size_t>(seedmax) * (L.Tws + 1) * ((m + 63) & ~63) * sizeof(float));
-  L.per_wg = L.off_rdist + al(static_cast<size_t>(m) * sizeof(float));
+  L.off_s64 = L.off_rdist + al(static_cast<size_t>(m) * sizeof(float));
+  L.off_c64 = L.off_s64 + al(static_cast<size_t>(L.Cws) * dpad * sizeof(double));
+  L.off_list = L.off_c64 + al(static_cast<size_t>(L.Cws) * sizeof(int));
+  L.lseg = list_seg(m);
+  L.per_wg = L.off_list + al(static_cast<size_t>(L.Pws) * NW * L.lseg * sizeof(uint2));
   return L;
 }
 
@@ -1868,6 +2085,10 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
   a.off_cpos = L.off_cpos;
   a.off_dbuf = L.off_dbuf;
   a.off_rdist = L.off_rdist;
+  a.off_s64 = L.off_s64;
+  a.off_c64 = L.off_c64;
+  a.off_list = L.off_list;
+  a.lseg = L.lseg;
   a.Pws = L.Pws;
   a.Kws = L.Kws;
   a.Tws = L.Tws;

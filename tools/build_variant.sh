@@ -1,0 +1,16 @@
+# Build a variant library from an alternative kmeans.hip (A/B runs through CCMI_LIB):
+#   bash tools/build_variant.sh NAME path/to/kmeans_variant.hip [extra HIPFLAGS]
+# -> consensus_clustering_amd/libccmi_NAME.so.  Builds in a private copy of the sources
+# (/tmp/ccmi_variant_NAME/consensus_clustering_amd/csrc), so variants can build in parallel.
+set -e
+NAME=$1; SRC=$(readlink -f "$2"); shift 2
+REPO=$(cd "$(dirname "$0")/.." && pwd)
+W=/tmp/ccmi_variant_$NAME
+rm -rf $W && mkdir -p $W/consensus_clustering_amd $W/include
+cp -r $REPO/consensus_clustering_amd/csrc $W/consensus_clustering_amd/
+cp $REPO/include/ccmi.h $W/include/
+cp "$SRC" $W/consensus_clustering_amd/csrc/kmeans.hip
+cd $W/consensus_clustering_amd/csrc
+make -j4 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $*" \
+  OUT=$REPO/consensus_clustering_amd/libccmi_$NAME.so BUILD=$W/build > $W/build.log 2>&1 || { tail -20 $W/build.log; exit 1; }
+echo built libccmi_$NAME.so

@@ -35,7 +35,7 @@ for r in range(reps + 1):
     if r:
         ts.append(a.elapsed_time(b))
 print(os.path.basename(os.environ.get("CCMI_LIB", "libccmi.so")), "kmeans ms", [round(t, 1) for t in ts],
-      "sweeps", int(bk.stats[4]), flush=True)
+      "sweeps", int(bk.stats[4]), "sparse item-sweeps", int(bk.stats[6]), "changes", int(bk.stats[7]), flush=True)
 st = bk.stats.cpu().numpy()
 cyc, cnt = st[80:89].astype(float), st[96:105].astype(float)
 tot = max(cyc.sum(), 1)
