@@ -349,6 +349,16 @@ class ConsensusClustering:
                        counts, M)
         return M, I_full
 
+    def _consensus_device(self, K):
+        """float32 C for one K on the device (the kept cij when the fit kept its matrices)."""
+        v = self.cdf_at_K_data[K]
+        if v.get('cij') is not None:
+            return torch.from_numpy(np.ascontiguousarray(v['cij'])).to(self.labels_.device)
+        M, I = self._device_counts(K)
+        C = engine.consensus(M, I)
+        del M, I
+        return C
+
     def consensus_matrix(self, K):
         """float32 C for one K (CC.py:372-373), recomputed on the GPU when not kept."""
         v = self.cdf_at_K_data[K]
@@ -383,7 +393,8 @@ class ConsensusClustering:
     # or below this (about 1 s of cc_kmeans_f64 at the measured ~1.3 ns per unit; C1 is 1.1e7)
     F64_AUTO_MAX_WORK = 7.5e8
 
-    # largest n for predict(): the linkage runs on the host over the n x n float64 distances
+    # largest n for predict() with linkage='single' (a host linkage over n x n float64 distances);
+    # 'average', 'complete' and 'weighted' run on the device for any n that fits in HBM
     PREDICT_MAX_N = 20000
 
     def predict(self, K=None, distance='manhattan'):
@@ -393,35 +404,48 @@ class ConsensusClustering:
         (`_get_consensus_labels`, CC.py:292-314): agglomerative clustering with
         ``agg_clustering_linkage`` of the ROWS of C under the manhattan metric
         (``AgglomerativeClustering(n_clusters=K, linkage=..., affinity='manhattan')``, CC.py:306-312;
-        sklearn >= 1.4 spells the keyword ``metric``).  The n x n manhattan distances are
-        computed on the GPU in float64 with scipy's summation order (cc_manhattan, bit-identical
-        to ``scipy.spatial.distance.pdist(C, 'cityblock')``), then the linkage runs on the host.
+        sklearn >= 1.4 spells the keyword ``metric``).  Everything runs on the GPU: C from the
+        label matrix (cc_coassoc, cc_consensus), the n x n manhattan distances in float64 with
+        scipy's summation order (cc_manhattan, bit-identical to
+        ``scipy.spatial.distance.pdist(C, 'cityblock')``), and for 'average', 'complete' and
+        'weighted' linkage scipy's nn_chain (cc_linkage_nnchain), whose merges the host sorts,
+        relabels and cuts as scipy's linkage() and sklearn's ``_hc_cut`` do.  n is bounded by HBM
+        (C, then 8 n^2 bytes of distances: 20 GB at n = 50 000).  'single' linkage keeps the host
+        path (sklearn's own minimum-spanning-tree code), for n <= PREDICT_MAX_N.
 
         distance='1-C' is an opt-in variant: the same linkage over 1 - C as a precomputed
         consensus distance.
-
-        The host linkage needs O(n^2) float64 memory, so n is capped at PREDICT_MAX_N.
         """
-        from sklearn.cluster import AgglomerativeClustering
-
         K = self.best_k_ if K is None else K
         n = self._N
-        if n > self.PREDICT_MAX_N:
-            raise ValueError(f"predict(): n = {n} > PREDICT_MAX_N = {self.PREDICT_MAX_N}; the "
-                             "host linkage needs n^2 float64 distances")
-        if self.agg_clustering_linkage == 'ward':
+        link = self.agg_clustering_linkage
+        if link == 'ward':
             raise ValueError("ward linkage needs the euclidean metric; the reference's manhattan "
                              "consensus linkage supports 'average', 'complete' and 'single'")
+        if distance not in ('manhattan', '1-C'):
+            raise ValueError("distance must be 'manhattan' or '1-C'")
+        if link in engine.LINKAGE_METHODS:
+            C = self._consensus_device(K)
+            if distance == 'manhattan':
+                D = engine.manhattan(C)
+            else:
+                D = 1.0 - C.double()
+            del C
+            Z = engine.linkage(D, link)
+            del D
+            return post.hc_cut(K, Z[:, :2].astype(np.int64), n)
+        from sklearn.cluster import AgglomerativeClustering
+
+        if n > self.PREDICT_MAX_N:
+            raise ValueError(f"predict(): n = {n} > PREDICT_MAX_N = {self.PREDICT_MAX_N} for linkage "
+                             f"'{link}' (host linkage over n^2 float64 distances)")
         C = self.consensus_matrix(K)
         if distance == 'manhattan':
             D = engine.manhattan(torch.from_numpy(np.ascontiguousarray(C)).to(self.labels_.device))
             D = D.cpu().numpy()
-        elif distance == '1-C':
-            D = 1.0 - C.astype(np.float64)
         else:
-            raise ValueError("distance must be 'manhattan' or '1-C'")
-        agg = AgglomerativeClustering(n_clusters=K, metric='precomputed',
-                                      linkage=self.agg_clustering_linkage)
+            D = 1.0 - C.astype(np.float64)
+        agg = AgglomerativeClustering(n_clusters=K, metric='precomputed', linkage=link)
         return agg.fit_predict(D)
 
     @property

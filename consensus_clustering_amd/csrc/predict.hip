@@ -97,3 +97,166 @@ extern "C" int cc_manhattan(const float* C, int n, int d, double* D, void* strea
   }
   return CC_OK;
 }
+
+// ---- Agglomerative linkage on the device: scipy.cluster.hierarchy.nn_chain
+// (scipy/cluster/_hierarchy.pyx, the algorithm linkage() runs for 'complete', 'average' and
+// 'weighted'), the tree AgglomerativeClustering cuts (CC.py:306-312 -> sklearn linkage_tree ->
+// hierarchy.linkage).  The same sequence of decisions as scipy's loop: the chain grows from the
+// first live cluster; a step's nearest neighbour of the chain top x is the first index (scan
+// order) of the minimum over live i != x of D[x, i], taken only when strictly below D[x, prev]
+// (so the previous chain element wins ties); mutual neighbours merge (x < y kept as in
+// fastcluster), the merged cluster takes y's row and column, x dies; the Lance-Williams update is
+// the float64 expression of _hierarchy_distance_update.pxi with no contraction.  One workgroup
+// runs the whole chain (every step is a scan or an update over n entries; the full symmetric
+// n x n float64 matrix stays in HBM: 20 GB at n = 50k).  Z is written in merge order, unsorted;
+// the host sorts it by distance (stable) and relabels, as linkage() does after nn_chain.
+namespace {
+
+constexpr int LT = 1024;  // threads of the linkage workgroup
+
+__device__ __forceinline__ double lw_update(int method, double dxi, double dyi, int nx, int ny) {
+#pragma clang fp contract(off)  // scipy's products and sum rounded separately (no FMA)
+  if (method == CC_LINK_COMPLETE) return dxi > dyi ? dxi : dyi;  // fmax(d_xi, d_yi)
+  if (method == CC_LINK_WEIGHTED) return 0.5 * (dxi + dyi);
+  // average: (size_x * d_xi + size_y * d_yi) / (size_x + size_y)
+  const double a = static_cast<double>(nx) * dxi;
+  const double b = static_cast<double>(ny) * dyi;
+  return (a + b) / static_cast<double>(nx + ny);
+}
+
+// Block minimum of (v, i): the lower value, ties to the lower index.
+__device__ __forceinline__ void block_argmin(double& v, int& i, double* rv, int* ri) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(v, o);
+    const int oi = __shfl_xor(i, o);
+    if (ov < v || (ov == v && oi < i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    rv[w] = v;
+    ri[w] = i;
+  }
+  __syncthreads();
+  v = rv[0];
+  i = ri[0];
+  for (int k = 1; k < LT / 64; ++k)
+    if (rv[k] < v || (rv[k] == v && ri[k] < i)) {
+      v = rv[k];
+      i = ri[k];
+    }
+}
+
+__global__ __launch_bounds__(LT) void nnchain_kernel(double* __restrict__ D, int n, int method,
+                                                     double* __restrict__ Z, int* __restrict__ size,
+                                                     int* __restrict__ chain) {
+  __shared__ double rv[LT / 64];
+  __shared__ int ri[LT / 64];
+  const int tid = threadIdx.x;
+  const size_t nn = static_cast<size_t>(n);
+  constexpr double INF = __builtin_huge_val();
+  for (int i = tid; i < n; i += LT) size[i] = 1;
+  __syncthreads();
+  int len = 0;  // uniform: every thread runs the same control flow
+  for (int k = 0; k < n - 1; ++k) {
+    if (len == 0) {  // the first live cluster
+      double v = INF;
+      int i0 = 0x7fffffff;
+      for (int i = tid; i < n; i += LT)
+        if (size[i] > 0) {
+          i0 = i;
+          v = 0.0;
+          break;
+        }
+      block_argmin(v, i0, rv, ri);
+      if (tid == 0) chain[0] = i0;
+      __syncthreads();
+      len = 1;
+    }
+    int x, y;
+    double cur;
+    for (;;) {
+      x = chain[len - 1];
+      y = -1;
+      cur = INF;
+      if (len > 1) {
+        y = chain[len - 2];
+        cur = D[x * nn + y];
+      }
+      const double* row = D + x * nn;
+      double v = INF;
+      int bi = 0x7fffffff;
+      for (int i = tid; i < n; i += LT) {
+        if (i == x || size[i] == 0) continue;
+        const double d = row[i];
+        if (d < v) {  // increasing i per thread: the first minimum
+          v = d;
+          bi = i;
+        }
+      }
+      block_argmin(v, bi, rv, ri);
+      if (v < cur) {
+        cur = v;
+        y = bi;
+      }
+      if (len > 1 && y == chain[len - 2]) break;
+      __syncthreads();  // every thread has read chain[len - 2] before it may be overwritten
+      if (tid == 0) chain[len] = y;
+      __syncthreads();
+      ++len;
+    }
+    len -= 2;
+    if (x > y) {
+      const int t = x;
+      x = y;
+      y = t;
+    }
+    const int nx = size[x], ny = size[y];
+    __syncthreads();  // every thread has read the sizes
+    if (tid == 0) {
+      Z[4 * static_cast<size_t>(k) + 0] = x;
+      Z[4 * static_cast<size_t>(k) + 1] = y;
+      Z[4 * static_cast<size_t>(k) + 2] = cur;
+      Z[4 * static_cast<size_t>(k) + 3] = nx + ny;
+      size[x] = 0;
+      size[y] = nx + ny;
+    }
+    __syncthreads();
+    const double* rx = D + x * nn;
+    double* ry = D + y * nn;
+    for (int i = tid; i < n; i += LT) {
+      if (i == y || size[i] == 0) continue;
+      const double nd = lw_update(method, rx[i], ry[i], nx, ny);
+      ry[i] = nd;
+      D[i * nn + y] = nd;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+extern "C" size_t cc_linkage_workspace_bytes(int n) {
+  return n > 0 ? 2 * static_cast<size_t>(n) * sizeof(int) : 0;
+}
+
+extern "C" int cc_linkage_nnchain(double* D, int n, int method, double* Z, void* workspace, size_t ws_bytes,
+                                  void* stream) {
+  if (!D || !Z || n < 2 || !workspace || ws_bytes < cc_linkage_workspace_bytes(n) ||
+      (method != CC_LINK_AVERAGE && method != CC_LINK_COMPLETE && method != CC_LINK_WEIGHTED)) {
+    cc::set_error("cc_linkage_nnchain: bad arguments");
+    return CC_ERR_ARG;
+  }
+  int* size = static_cast<int*>(workspace);
+  hipLaunchKernelGGL(nnchain_kernel, dim3(1), dim3(LT), 0, static_cast<hipStream_t>(stream), D, n, method, Z, size,
+                     size + n);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cc::set_error(std::string("cc_linkage_nnchain: ") + hipGetErrorString(e));
+    return CC_ERR_HIP;
+  }
+  return CC_OK;
+}

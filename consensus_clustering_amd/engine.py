@@ -229,6 +229,33 @@ def consensus(M: torch.Tensor, I: torch.Tensor) -> torch.Tensor:
     return C
 
 
+LINKAGE_METHODS = {"average": 0, "complete": 1, "weighted": 2}  # CC_LINK_* (include/ccmi.h)
+
+
+def linkage_raw(D: torch.Tensor, method: str) -> torch.Tensor:
+    """nn_chain's merges (x, y, distance, size) in merge order, on the device (D overwritten)."""
+    assert D.dtype == torch.float64 and D.dim() == 2 and D.shape[0] == D.shape[1] and D.is_contiguous()
+    n = D.shape[0]
+    Z = torch.empty((n - 1, 4), dtype=torch.float64, device=D.device)
+    lib = _lib.load()
+    ws = torch.empty(int(lib.cc_linkage_workspace_bytes(n)), dtype=torch.uint8, device=D.device)
+    _lib.call("cc_linkage_nnchain", D.data_ptr(), n, LINKAGE_METHODS[method], Z.data_ptr(), ws.data_ptr(),
+              ws.numel(), stream_ptr())
+    return Z
+
+
+def linkage(D: torch.Tensor, method: str) -> np.ndarray:
+    """scipy.cluster.hierarchy.linkage of the symmetric float64 [n, n] distances D (device; D is
+    overwritten) for method in LINKAGE_METHODS: scipy's nn_chain on the device
+    (cc_linkage_nnchain), then linkage()'s stable sort of the merges by distance and its union-find
+    relabelling (scipy/cluster/_hierarchy.pyx: nn_chain, label) on the host.  Returns Z [n-1, 4]."""
+    n = D.shape[0]
+    Z = linkage_raw(D, method)
+    from .post import linkage_finish
+
+    return linkage_finish(Z.cpu().numpy(), n)
+
+
 def manhattan(C: torch.Tensor) -> torch.Tensor:
     """float64 [n, n] manhattan distances between the rows of the float32 [n, n] C."""
     assert C.dtype == torch.float32 and C.dim() == 2 and C.is_contiguous()

@@ -77,3 +77,56 @@ def best_k(pac: dict):
     if not Ks:
         return None
     return Ks[int(np.argmin(np.array([pac[K] for K in Ks], dtype=np.float64)))]
+
+
+def linkage_finish(Z, n):
+    """scipy linkage()'s last steps on nn_chain's raw merges Z [n-1, 4] (x, y, distance, size in
+    merge order): a stable sort by distance, then label() (scipy/cluster/_hierarchy.pyx): with a
+    union-find, each merge's two clusters are renamed to their current roots (smaller first) and
+    the merge creates cluster n + i."""
+    Z = np.asarray(Z, dtype=np.float64)
+    Z = Z[np.argsort(Z[:, 2], kind="mergesort")].copy()
+    parent = list(range(2 * n - 1))
+    size = [1] * (2 * n - 1)
+
+    def find(x):
+        r = x
+        while parent[r] != r:
+            r = parent[r]
+        while parent[x] != r:
+            parent[x], x = r, parent[x]
+        return r
+
+    for i in range(n - 1):
+        xr, yr = find(int(Z[i, 0])), find(int(Z[i, 1]))
+        Z[i, 0], Z[i, 1] = (xr, yr) if xr < yr else (yr, xr)
+        parent[xr] = parent[yr] = n + i
+        size[n + i] = size[xr] + size[yr]
+        Z[i, 3] = size[n + i]
+    return Z
+
+
+def hc_cut(n_clusters, children, n_leaves):
+    """Labels of the n_clusters-cluster cut of a linkage tree, as AgglomerativeClustering assigns
+    them (sklearn/cluster/_agglomerative.py `_hc_cut`: a max-heap of node ids, each step
+    replacing the largest by its two children; label i for the descendants of the i-th heap
+    entry).  children: int [n_leaves - 1, 2] (linkage Z[:, :2])."""
+    import heapq
+
+    children = np.asarray(children, dtype=np.int64)
+    nodes = [-(int(max(children[-1])) + 1)]
+    for _ in range(n_clusters - 1):
+        these = children[-nodes[0] - n_leaves]
+        heapq.heappush(nodes, -int(these[0]))
+        heapq.heappushpop(nodes, -int(these[1]))
+    label = np.zeros(n_leaves, dtype=np.intp)
+    for i, node in enumerate(nodes):
+        stack, leaves = [-node], []
+        while stack:
+            v = stack.pop()
+            if v < n_leaves:
+                leaves.append(v)
+            else:
+                stack.extend(children[v - n_leaves])
+        label[leaves] = i
+    return label

@@ -160,6 +160,19 @@ int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C, void* stre
  * under the manhattan metric). */
 int cc_manhattan(const float* C, int n, int d, double* D, void* stream);
 
+/* Agglomerative linkage of the consensus labels (CC.py:306-312: AgglomerativeClustering ->
+ * sklearn linkage_tree -> scipy.cluster.hierarchy.linkage -> _hierarchy.nn_chain) on the device:
+ * D [n][n] float64 symmetric (e.g. from cc_manhattan) is overwritten; Z [n-1][4] float64 receives
+ * (x, y, distance, size) per merge in nn_chain's merge order, before linkage()'s stable sort by
+ * distance and relabelling (done by the caller).  One workgroup; workspace of
+ * cc_linkage_workspace_bytes(n) bytes. */
+#define CC_LINK_AVERAGE 0
+#define CC_LINK_COMPLETE 1
+#define CC_LINK_WEIGHTED 2
+size_t cc_linkage_workspace_bytes(int n);
+int cc_linkage_nnchain(double* D, int n, int method, double* Z, void* workspace, size_t ws_bytes,
+                       void* stream);
+
 /* Batched k-means for every (resample h, K, init) problem, replacing the per-(K, h)
  * clusterer.fit_predict(X[indices]) of CC.py:282 for the default clusterer
  * (sklearn KMeans: k-means++ init with 2+floor(ln K) local trials, Lloyd with strict

@@ -1,0 +1,77 @@
+"""Device linkage of predict() (cc_linkage_nnchain): its raw merges equal the oracle's
+restatement of scipy's nn_chain bit for bit (ties included), and predict() runs at the headline
+n = 50 000 (CC.py:292-314), recovering a planted block structure."""
+import time
+
+import numpy as np
+import pytest
+import torch
+from scipy.spatial.distance import pdist, squareform
+
+from consensus_clustering_amd import engine, post
+from oracle import cc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _distances(n, seed, ties=False):
+    rs = np.random.RandomState(seed)
+    X = rs.rand(n, 6).astype(np.float32)
+    if ties:
+        X = np.round(X * 3) / 3
+        X[n // 2:] = X[: n - n // 2]
+    return squareform(pdist(X, "cityblock"))
+
+
+@pytest.mark.parametrize("method", ["average", "complete", "weighted"])
+@pytest.mark.parametrize("n,seed,ties", [(2, 0, False), (3, 0, True), (257, 1, True), (1500, 2, False)])
+def test_device_nn_chain_equals_oracle(method, n, seed, ties):
+    D = _distances(n, seed, ties)
+    want = O.nn_chain(D, method)
+    got = engine.linkage_raw(torch.from_numpy(D).cuda(), method).cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+
+
+def test_device_linkage_on_manhattan_of_consensus_rows():
+    """The predict() chain on a consensus-like C: manhattan on the device, then the linkage;
+    equal to scipy's linkage of pdist(C, 'cityblock')."""
+    from scipy.cluster.hierarchy import linkage
+
+    rs = np.random.RandomState(5)
+    n, k = 900, 4
+    g = rs.randint(0, k, n)
+    C = (g[:, None] == g[None, :]).astype(np.float32) * 0.8 + rs.rand(n, n).astype(np.float32) * 0.2
+    C = np.ascontiguousarray(np.minimum(C, C.T))
+    np.fill_diagonal(C, 1.0)
+    D = engine.manhattan(torch.from_numpy(C).cuda())
+    Z = engine.linkage(D, "average")
+    np.testing.assert_array_equal(Z, linkage(pdist(C, "cityblock"), method="average"))
+
+
+def test_predict_headline_n():
+    """n = 50 000 (BASELINE configs[2]): C with 6 planted blocks (co-clustering 0.9 inside a
+    block, 0.1 across, noise) -> manhattan (float64) -> average linkage, all on the device; the
+    cut at K = 6 recovers the blocks.  Prints the stage times."""
+    n, k = 50_000, 6
+    dev = torch.device("cuda")
+    g = torch.randint(0, k, (n,), generator=torch.Generator().manual_seed(0)).to(dev)
+    C = torch.where(g[:, None] == g[None, :], 0.9, 0.1).float()
+    C += torch.rand((n, n), generator=torch.Generator(device=dev).manual_seed(1), device=dev) * 0.05
+    C = torch.minimum(C, C.T).contiguous()
+    C.fill_diagonal_(1.0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    D = engine.manhattan(C)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    del C
+    Z = engine.linkage(D, "average")
+    t2 = time.perf_counter()
+    del D
+    lab = post.hc_cut(k, Z[:, :2].astype(np.int64), n)
+    t3 = time.perf_counter()
+    print(f"predict n={n}: manhattan {t1 - t0:.2f} s, linkage {t2 - t1:.2f} s, cut {t3 - t2:.2f} s")
+    gh = g.cpu().numpy()
+    # the cut's clusters are the planted blocks (a bijection)
+    pairs = set(zip(lab.tolist(), gh.tolist()))
+    assert len(pairs) == k and len({a for a, _ in pairs}) == k and len({b for _, b in pairs}) == k
