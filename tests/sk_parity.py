@@ -3,10 +3,14 @@ KMeans called as CC.py:205-214 / :282 call it.  Not a test module."""
 import numpy as np
 
 
-def _fixed_point_no_worse(rows, got, ref, K, rel=1e-6):
+def _fixed_point_no_worse(rows, got, ref, K, rel=1e-4):
     """The engine's labels `got` are a Lloyd fixed point in float64 (centres = means of its
     clusters; every row's nearest centre, lowest index on ties, is its own) and their inertia is
-    at most sklearn's (labels `ref`) times 1 + rel."""
+    at most sklearn's (labels `ref`) times 1 + rel: a converged solution of the same quality
+    reached along a trajectory that rounding moved.  rel = 1e-4: at C2 K = 8 (resample 3) the
+    engine and sklearn's best init run the same 20 iterations and end 23 boundary rows apart, both
+    fixed points, inertias within 1e-4; distinct local optima of that problem differ by ~8e-4
+    (profiles/r03/parity_diag_c2_K8_h3.txt)."""
     X = rows.astype(np.float64)
 
     def centres(lab):
@@ -92,7 +96,7 @@ def sklearn_parity(X, labels, idx, Ks, seed, resamples, skip=0, threads=16, n_in
                     unexplained.append((K, h, float(np.mean(ref32 == got))))
     total = len(Ks) * resamples
     print(f"sklearn parity: {same}/{total} identical, {explained} differ where sklearn's own float32 "
-          f"fit is rounding-sensitive ({fixed} of them shown as a float64 Lloyd fixed point of equal or "
-          f"lower inertia), {len(unexplained)} unexplained {unexplained}")
+          f"fit is rounding-sensitive ({fixed} of them shown as a float64 Lloyd fixed point of inertia "
+          f"within 1e-4 of sklearn's), {len(unexplained)} unexplained {unexplained}")
     assert len(unexplained) <= max_unexplained, unexplained
     return same, explained, total

@@ -2,7 +2,8 @@
 inertia against each of sklearn's n_init runs (same k-means++ stream, replicated with sklearn's
 own _kmeans_plusplus / _kmeans_single_lloyd).
 
-    python tools/diag_parity.py n d k_true K h H seed
+    python tools/diag_parity.py n d k_true K h H seed [bench]
+(`bench`: the rows of bench.make_blobs_f32(n, d, k_true, seed), the data of the scale tests.)
 """
 import os
 import sys
@@ -20,9 +21,14 @@ from consensus_clustering_amd import engine  # noqa: E402
 from consensus_clustering_amd.kmeans import BatchedKMeans, prepare_rows  # noqa: E402
 
 n, d, k, K, h, H, seed = (int(v) for v in sys.argv[1:8])
-X, _ = make_blobs(n_samples=n, n_features=d, centers=k, cluster_std=1.0, center_box=(-10, 10), shuffle=True,
-                  random_state=n)
-X = X.astype(np.float32)
+if len(sys.argv) > 8 and sys.argv[8] == "bench":
+    from bench import make_blobs_f32
+
+    X = make_blobs_f32(n, d, k, seed=seed)
+else:
+    X, _ = make_blobs(n_samples=n, n_features=d, centers=k, cluster_std=1.0, center_box=(-10, 10), shuffle=True,
+                      random_state=n)
+    X = X.astype(np.float32)
 m = int(0.8 * n)
 idx = engine.resample_indices(seed, n, m, 0, H)
 dev = engine.require_gpu()
@@ -47,3 +53,17 @@ with threadpool_limits(4):
         lab, ine, cen, it = _kmeans_single_lloyd(Xc, sw, c0, max_iter=300, tol=tol, n_threads=4)
         print(f"sklearn init {i}: inertia {ine:.6f} n_iter {it} seeds {sorted(ci.tolist())[:10]} "
               f"label agreement with engine {np.mean(lab == got):.4f}")
+
+from sklearn.cluster import KMeans  # noqa: E402
+
+for th in (1, 4, 16):
+    with threadpool_limits(th):
+        ref = KMeans(n_clusters=K, random_state=seed, n_init=3).fit(rows)
+    print(f"sklearn KMeans f32 threads={th}: inertia {ref.inertia_:.6f} agreement with engine "
+          f"{np.mean(ref.labels_ == got):.5f}")
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from sk_parity import _fixed_point_no_worse  # noqa: E402
+
+print("engine partition a float64 Lloyd fixed point no worse than sklearn:",
+      _fixed_point_no_worse(rows, got, ref.labels_, K), "| with 1e-4 slack:",
+      _fixed_point_no_worse(rows, got, ref.labels_, K, rel=1e-4))
