@@ -133,10 +133,12 @@ def cpu_baseline(cfg, X, H_sample=8):
     Hs = min(H, H_sample)
     idx = O.subsampling_indices(n, Hs, frac, SEED)
     t0 = time.perf_counter()
+    print(f"[bench] cpu baseline: {cores} joblib processes", file=sys.stderr, flush=True)
     with Parallel(n_jobs=cores, prefer="processes") as par:
         a = time.perf_counter()
         par(delayed(_timed_fit)(X, idx[h], K) for K in Ks for h in range(Hs))
         T_fits = (time.perf_counter() - a) * (H / Hs)
+        print("[bench] cpu baseline: fits sampled", file=sys.stderr, flush=True)
         block = min(n, 1000)
         sampleK = sorted({Ks[0], Ks[len(Ks) // 2], Ks[-1]})
         tco = par(delayed(_timed_coassoc)(n, idx[0], K, K, block) for K in sampleK)
@@ -149,6 +151,7 @@ def cpu_baseline(cfg, X, H_sample=8):
         a = time.perf_counter()
         np.dot(S[:, :bI].T, S)
         T_I = (time.perf_counter() - a) * (n / bI)
+        print("[bench] cpu baseline: S^T S sampled", file=sys.stderr, flush=True)
         bA = min(n, 500)
         M = np.random.RandomState(1).randint(0, H + 1, size=(bA, n), dtype=S.dtype)
         I = np.maximum(M, H // 2).astype(S.dtype)
@@ -175,11 +178,28 @@ def cpu_baseline(cfg, X, H_sample=8):
 
 
 def usable_cores() -> int:
-    """CPUs this process may run on (its affinity mask), not the machine's total."""
+    """CPUs this process may use: its affinity mask, capped by the cgroup CPU quota (a GPU box
+    shows every host CPU in the mask but grants one GPU's share of them)."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover - non-Linux
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    quota = None
+    try:  # cgroup v2
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return n
 
 
 def band_pairs(n: int, tile_begin: int, tile_end: int, T: int = 256) -> int:
