@@ -103,6 +103,11 @@ constexpr int US = CC_KM_USTRIDE;
 #ifndef KM_COST_DIST_NARROW
 #define KM_COST_DIST_NARROW KM_COST_DIST * DP / 128
 #endif
+// The sparse M-step pays at d = 128 only: at d = 32 / 64 the M-step MFMAs it removes are cheap
+// (one or two 32-dim blocks) against the post-sweep work that grows with m (C5 k-means 314 ->
+// 538 ms with it, C2 89 -> 92 ms).
+template <int DP>
+constexpr bool kSparse = DP == 128;
 // The distance waves' starting cost per active slot tile for feature padding DP.
 template <int DP>
 __host__ __device__ constexpr int dist_cost() { return KM_COST_DIST_NARROW; }
@@ -1092,7 +1097,7 @@ __device__ __forceinline__ void msum_out(const KArgs& a, State& S, float* Sm, co
 // Thread 0: admit waiting problems into free seeding slots, then pack the next sweep:
 // seeding candidates first (they are on every problem's critical path), then Lloyd
 // problems round-robin from S.rr, first fit into the CW slots.
-__device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_cost) {
+__device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_cost, bool sparse_ok) {
   const int P = S.P;
   for (int p = 0; p < P && S.seedfree; ++p) {
     if (S.st[p] != ST_WAIT) continue;
@@ -1155,7 +1160,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_
     const int kind = (st == ST_RUN) ? IK_RUN : IK_FINAL;
     // sparse: the sums follow the labels that changed (few moved in the last E-step; no M-step
     // MFMAs); dense: the M-step recomputes them (the first iteration, after a burst of changes)
-    const bool sparse = st == ST_RUN && S.pchg[p] <= a.m / 8;
+    const bool sparse = sparse_ok && st == ST_RUN && S.pchg[p] <= a.m / 8;
     S.isparse[ni] = static_cast<unsigned char>(sparse);
     S.ikind[ni] = static_cast<unsigned char>(kind);
     S.iprob[ni] = static_cast<unsigned char>(p);
@@ -1334,7 +1339,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     // ---- sweeps -----------------------------------------------------------------
     for (;;) {
       KM_STAMP(swp);
-      if (tid == 0) schedule(a, S, idx, dist_cost<DP>());
+      if (tid == 0) schedule(a, S, idx, dist_cost<DP>(), kSparse<DP>);
       __syncthreads();
       const int nitems = S.nitems, ncols = S.ncols;
       if (nitems == 0) break;
@@ -1594,28 +1599,45 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       // one, each wave over its eighth of the rows; the changed rows of a sparse item go to its
       // change list (a dense item's are only counted); then this sweep's buffer becomes the
       // current one
-      for (int it = 0; it < nitems; ++it) {
-        if (S.ikind[it] != IK_RUN) continue;
-        const int p = S.iprob[it];
-        const uint8_t* cur = glab + static_cast<size_t>(2 * p + 1 - S.lcur[p]) * a.lsm;
-        const uint8_t* old = glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm;
-        const unsigned nc = list_changes(cur, old, m, wave, lane, clist + (static_cast<size_t>(p) * NW + wave) * a.lseg,
-                                         S.isparse[it] ? static_cast<unsigned>(a.lseg) : 0u);
-        if (lane == 0) S.lcnt[it][wave] = nc;
-      }
-      __syncthreads();
-      if (tid < nitems) {
-        const int it = tid;
-        S.ichanged[it] = 0;
-        if (S.ikind[it] == IK_RUN) {
-          unsigned tot = 0;
-          bool over = false;
-          for (int w = 0; w < NW; ++w) {
-            tot += S.lcnt[it][w];
-            over |= S.lcnt[it][w] > static_cast<unsigned>(a.lseg);
+      if constexpr (kSparse<DP>) {
+        for (int it = 0; it < nitems; ++it) {
+          if (S.ikind[it] != IK_RUN) continue;
+          const int p = S.iprob[it];
+          const uint8_t* cur = glab + static_cast<size_t>(2 * p + 1 - S.lcur[p]) * a.lsm;
+          const uint8_t* old = glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm;
+          const unsigned nc = list_changes(cur, old, m, wave, lane, clist + (static_cast<size_t>(p) * NW + wave) * a.lseg,
+                                           S.isparse[it] ? static_cast<unsigned>(a.lseg) : 0u);
+          if (lane == 0) S.lcnt[it][wave] = nc;
+        }
+        __syncthreads();
+        if (tid < nitems) {
+          const int it = tid;
+          S.ichanged[it] = 0;
+          if (S.ikind[it] == IK_RUN) {
+            unsigned tot = 0;
+            bool over = false;
+            for (int w = 0; w < NW; ++w) {
+              tot += S.lcnt[it][w];
+              over |= S.lcnt[it][w] > static_cast<unsigned>(a.lseg);
+            }
+            S.pchg[S.iprob[it]] = static_cast<int>(tot);
+            S.ichanged[it] = (tot != 0) | ((S.isparse[it] && over) ? 2u : 0u);  // 2: rebuild the sums
           }
-          S.pchg[S.iprob[it]] = static_cast<int>(tot);
-          S.ichanged[it] = (tot != 0) | ((S.isparse[it] && over) ? 2u : 0u);  // 2: rebuild the sums
+        }
+      } else {  // flags only: 16 B per thread and load, every item in one pass
+        if (tid < nitems) S.ichanged[tid] = 0;
+        __syncthreads();
+        for (int it = 0; it < nitems; ++it) {
+          if (S.ikind[it] != IK_RUN) continue;
+          const int p = S.iprob[it];
+          const uint4* cur = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + 1 - S.lcur[p]) * a.lsm);
+          const uint4* old = reinterpret_cast<const uint4*>(glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm);
+          bool diff = false;
+          for (int e = tid; e < (m + 15) / 16; e += NT) {
+            const uint4 x = cur[e], y = old[e];
+            diff |= (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
+          }
+          if (diff) S.ichanged[it] = 1;
         }
       }
       __syncthreads();
@@ -1627,45 +1649,47 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           }
       __syncthreads();
 
-      // ---- running sums: dense items take the M-step's sums; sparse items add their change
-      // lists (one wave per item) into the f64 sums, which then feed the centre update below
-      for (int e = tid; e < ncols * DP; e += NT) {
-        const int sl = e / DP, d = e - sl * DP;
-        const int it = S.sitem[sl];
-        if (it < 0 || S.ikind[it] != IK_RUN || S.isparse[it] || sl - S.ioff[it] >= S.K[S.iprob[it]]) continue;
-        const int row = S.cenoff[S.iprob[it]] + (sl - S.ioff[it]);
-        s64[static_cast<size_t>(row) * DP + d] = static_cast<double>(Sm[e]);
-        if (d == 0) c64[row] = static_cast<int>(S.cnt[sl]);
-      }
-      {
-        int j = 0;
-        for (int it = 0; it < nitems; ++it) {
-          if (S.ikind[it] != IK_RUN || !S.isparse[it]) continue;
-          if ((j++ % NW) != wave) continue;
-          const int p = S.iprob[it], off = S.ioff[it];
-          apply_changes<DP>(a, idx, clist + static_cast<size_t>(p) * NW * a.lseg, S.lcnt[it], (S.ichanged[it] & 2u) != 0,
-                            glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm, Sm + static_cast<size_t>(off) * DP,
-                            S.cnt + off, S.K[p], lane);
+      // ---- running sums (d = 128): dense items take the M-step's sums; sparse items add their
+      // change lists (one wave per item) into the f64 sums, which then feed the centre update below
+      if constexpr (kSparse<DP>) {
+        for (int e = tid; e < ncols * DP; e += NT) {
+          const int sl = e / DP, d = e - sl * DP;
+          const int it = S.sitem[sl];
+          if (it < 0 || S.ikind[it] != IK_RUN || S.isparse[it] || sl - S.ioff[it] >= S.K[S.iprob[it]]) continue;
+          const int row = S.cenoff[S.iprob[it]] + (sl - S.ioff[it]);
+          s64[static_cast<size_t>(row) * DP + d] = static_cast<double>(Sm[e]);
+          if (d == 0) c64[row] = static_cast<int>(S.cnt[sl]);
         }
-      }
-      __syncthreads();
-      for (int e = tid; e < ncols * DP; e += NT) {  // sparse items: f64 sums += the f32 deltas
-        const int sl = e / DP, d = e - sl * DP;
-        const int it = S.sitem[sl];
-        if (it < 0 || S.ikind[it] != IK_RUN || !S.isparse[it] || sl - S.ioff[it] >= S.K[S.iprob[it]]) continue;
-        const int row = S.cenoff[S.iprob[it]] + (sl - S.ioff[it]);
-        const bool full = (S.ichanged[it] & 2u) != 0;
-        double* sp = s64 + static_cast<size_t>(row) * DP + d;
-        const double t = (full ? 0.0 : *sp) + static_cast<double>(Sm[e]);
-        *sp = t;
-        Sm[e] = static_cast<float>(t);
-        if (d == 0) {
-          const int c = (full ? 0 : c64[row]) + static_cast<int>(S.cnt[sl]);
-          c64[row] = c;
-          S.cnt[sl] = static_cast<unsigned>(c);
+        {
+          int j = 0;
+          for (int it = 0; it < nitems; ++it) {
+            if (S.ikind[it] != IK_RUN || !S.isparse[it]) continue;
+            if ((j++ % NW) != wave) continue;
+            const int p = S.iprob[it], off = S.ioff[it];
+            apply_changes<DP>(a, idx, clist + static_cast<size_t>(p) * NW * a.lseg, S.lcnt[it], (S.ichanged[it] & 2u) != 0,
+                              glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm, Sm + static_cast<size_t>(off) * DP,
+                              S.cnt + off, S.K[p], lane);
+          }
         }
+        __syncthreads();
+        for (int e = tid; e < ncols * DP; e += NT) {  // sparse items: f64 sums += the f32 deltas
+          const int sl = e / DP, d = e - sl * DP;
+          const int it = S.sitem[sl];
+          if (it < 0 || S.ikind[it] != IK_RUN || !S.isparse[it] || sl - S.ioff[it] >= S.K[S.iprob[it]]) continue;
+          const int row = S.cenoff[S.iprob[it]] + (sl - S.ioff[it]);
+          const bool full = (S.ichanged[it] & 2u) != 0;
+          double* sp = s64 + static_cast<size_t>(row) * DP + d;
+          const double t = (full ? 0.0 : *sp) + static_cast<double>(Sm[e]);
+          *sp = t;
+          Sm[e] = static_cast<float>(t);
+          if (d == 0) {
+            const int c = (full ? 0 : c64[row]) + static_cast<int>(S.cnt[sl]);
+            c64[row] = c;
+            S.cnt[sl] = static_cast<unsigned>(c);
+          }
+        }
+        __syncthreads();
       }
-      __syncthreads();
 
       // ---- Lloyd M-step completion (RUN items) ------------------------------------
       if (tid == 0) {
@@ -1889,11 +1913,13 @@ WsLayout ws_layout(int m, int dpad, const int32_t* units, int nU, int seedmax) {
   L.off_cpos = L.off_cenn + al(static_cast<size_t>(L.Cws) * sizeof(float));
   L.off_dbuf = L.off_cpos + al(static_cast<size_t>(L.Pws) * L.Kws * sizeof(int32_t));
   L.off_rdist = L.off_dbuf + al(static_cast<size_t>(seedmax) * (L.Tws + 1) * ((m + 63) & ~63) * sizeof(float));
+  // the sparse M-step's running sums, counts and change lists (d = 128 only, kSparse)
+  const bool sp = dpad == 128;
   L.off_s64 = L.off_rdist + al(static_cast<size_t>(m) * sizeof(float));
-  L.off_c64 = L.off_s64 + al(static_cast<size_t>(L.Cws) * dpad * sizeof(double));
-  L.off_list = L.off_c64 + al(static_cast<size_t>(L.Cws) * sizeof(int));
+  L.off_c64 = L.off_s64 + (sp ? al(static_cast<size_t>(L.Cws) * dpad * sizeof(double)) : 0);
+  L.off_list = L.off_c64 + (sp ? al(static_cast<size_t>(L.Cws) * sizeof(int)) : 0);
   L.lseg = list_seg(m);
-  L.per_wg = L.off_list + al(static_cast<size_t>(L.Pws) * NW * L.lseg * sizeof(uint2));
+  L.per_wg = L.off_list + (sp ? al(static_cast<size_t>(L.Pws) * NW * L.lseg * sizeof(uint2)) : 0);
   return L;
 }
 
