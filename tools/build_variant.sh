@@ -10,6 +10,10 @@ rm -rf $W && mkdir -p $W/consensus_clustering_amd $W/include
 cp -r $REPO/consensus_clustering_amd/csrc $W/consensus_clustering_amd/
 cp $REPO/include/ccmi.h $W/include/
 cp "$SRC" $W/consensus_clustering_amd/csrc/kmeans.hip
+mkdir -p $W/build
+cp $REPO/build/ccmi/*.o $W/build/ 2>/dev/null || true  # unchanged objects are reused (kmeans.o rebuilds)
+rm -f $W/build/kmeans.o
+touch $W/build/*.o 2>/dev/null || true
 cd $W/consensus_clustering_amd/csrc
 make -j4 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $*" \
   OUT=$REPO/consensus_clustering_amd/libccmi_$NAME.so BUILD=$W/build > $W/build.log 2>&1 || { tail -20 $W/build.log; exit 1; }
