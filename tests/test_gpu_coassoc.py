@@ -97,6 +97,40 @@ def test_random_labels_vs_oracle(n, H, frac, Ks):
         np.testing.assert_array_equal(counts[j], pair)
 
 
+def test_cosampling_count_at_H_256():
+    """Co-sampling counts at the top of the range: rows 0..399 are in every one of H = 256
+    resamples (i = H), rows 0..149 keep one label each (m = i = 256), rows 0 and 1 never share a
+    label (m = 0 with i = 256)."""
+    dev = engine.require_gpu()
+    n, H, m, Ks = 600, 256, 500, [2, 3, 7]
+    rng = np.random.default_rng(11)
+    idx = np.stack([np.r_[np.arange(400), 400 + rng.permutation(200)[:100]] for _ in range(H)]).astype(np.int32)
+    labs = []
+    for K in Ks:
+        lab = rng.integers(0, K, size=(H, m)).astype(np.int32)
+        lab[:, :150] = rng.integers(0, 2, size=150)  # rows 0..149: one label each (m = 256)
+        lab[:, 0] = np.arange(H) % K
+        lab[:, 1] = (np.arange(H) + 1) % K
+        labs.append(lab)
+    L, Hpad = _device_labels(idx, labs, n, H, dev)
+    assert Hpad == 256
+    I_ref = O.cosample_matrix(idx.astype(np.int64), n)
+    assert I_ref[0, 1] == 256 and I_ref[0, 399] == 256
+    iu = np.triu_indices(n, 1)
+    for want_full in (False, True):
+        I, Ms, counts = _run(L, n, Hpad, Ks, want_full=want_full)
+        for j, K in enumerate(Ks):
+            M_ref = O.coassoc_matrix(idx.astype(np.int64), labs[j].astype(np.int64), K, n)
+            assert M_ref[0, 1] == 0 and M_ref[2, 3] in (0, 256)
+            C = O.consensus_matrix(M_ref.astype(np.uint16), I_ref.astype(np.uint16))
+            pair, _ = np.histogram(C[iu], bins=20, range=(0, 1))
+            np.testing.assert_array_equal(counts[j], pair, err_msg=f"K={K} want_full={want_full}")
+            if want_full:
+                np.testing.assert_array_equal(Ms[j], M_ref)
+        if want_full:
+            np.testing.assert_array_equal(I, I_ref)
+
+
 def test_tile_range_sharding_is_exact():
     """Row-band sharding of the triangle (multi-GPU mode B) sums to the single-range result."""
     dev = engine.require_gpu()

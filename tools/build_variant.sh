@@ -10,9 +10,10 @@ rm -rf $W && mkdir -p $W/consensus_clustering_amd $W/include
 cp -r $REPO/consensus_clustering_amd/csrc $W/consensus_clustering_amd/
 cp $REPO/include/ccmi.h $W/include/
 cp "$SRC" $W/consensus_clustering_amd/csrc/kmeans.hip
+[ -n "$CO_SRC" ] && cp "$CO_SRC" $W/consensus_clustering_amd/csrc/coassoc.hip  # a coassoc.hip variant (with REBUILD=coassoc)
 mkdir -p $W/build
 cp $REPO/build/ccmi/*.o $W/build/ 2>/dev/null || true  # unchanged objects are reused (kmeans.o rebuilds)
-rm -f $W/build/kmeans.o
+for o in kmeans $REBUILD; do rm -f $W/build/$o.o; done  # REBUILD="coassoc ...": objects whose flags change
 touch $W/build/*.o 2>/dev/null || true
 cd $W/consensus_clustering_amd/csrc
 make -j4 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $*" \
