@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -116,6 +117,7 @@ struct WArgs {
   int32_t* niter_out;
   unsigned long long* stats;
   int* active;             // scheduled column tiles of the next round (summed by P)
+  int reloc_full;          // diagnostics (CCMI_WIDE_RELOC_FULL): relocation reads every row exactly
   uint8_t* ws;
   size_t ws_per, off_tolp, off_tiles, off_part, off_glab, off_dbuf, off_cpos, off_cen, off_cenhl, off_cenn, off_rdist;
 };
@@ -391,6 +393,9 @@ __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
       if (ok) {
         R.glab[(static_cast<size_t>(p) * 2 + iw_buf(w0)) * a.lsm + r] = static_cast<uint8_t>(lab);
         v = static_cast<double>(xnr) + static_cast<double>(best);
+        // the row's squared distance to its centre as the E-step has it (dbuf slot 0 is free once
+        // a problem runs Lloyd): relocate() filters its candidates with it
+        R.dbuf[static_cast<size_t>(p) * a.ndb * a.lsm + r] = xnr + best;
       }
     } else {
       const float dist = fmaxf(xnr + drow[off], 0.f);
@@ -778,16 +783,76 @@ __device__ void update_row(const WArgs& a, float* nw, const float* od, float alp
 }
 
 // Empty-cluster relocation for problem p (rare; _k_means_common.pyx:167-212).  sums: the
-// problem's un-averaged sums [K][dpad]; cold: the centres the labels came from.
+// problem's un-averaged sums [K][dpad]; cold: the centres the labels came from; est: the E-step's
+// squared distance of each row to its centre, cn: the squared norms of cold.
+//
+// The clusters take the farthest rows by the exact distance (f64 sum of the f32 squared
+// differences, below), which reads every row in full: 320 MB per problem at C4, one workgroup,
+// ~25 ms.  Only rows that can be among the ne farthest are read: |est - exact| <= b_r with
+//   b_r = (2 d + 64) 2^-24 (|x| + |c|)^2 + 2^-22 sqrt(d) (|x| + |c|) / scale
+// (f32 accumulation of the f16 hi/lo products over d terms, their 2^-22 split error, the f32
+// norms and the f16 subnormal spacing of the scaled operands; the exact value's own rounding is
+// below the first term), so a row whose est + b_r is below the ne-th largest est - b is never
+// picked, and the candidates get their exact distance; the rest are excluded (-2).
 __device__ void relocate(const WArgs& a, PS& L, const int32_t* idx, int p, float* sums, const float* cold,
-                         const uint8_t* lab, float* dist, int tid) {
+                         const uint8_t* lab, const float* est, const float* cn, float* dist, int tid) {
   WProb& q = L.S.pr[p];
   const int m = a.m, K = q.K, dpad = a.dpad, off = q.cenoff;
-  // squared distance of every row to the centre it was assigned to: one wave per row,
-  // coalesced 16-B reads, f64 sum of the f32 squared differences
   const int lane = tid & 63, wave = tid >> 6, n4 = dpad / 4;
+  const float gam = static_cast<float>((2.0 * a.dreal + 64.0) * 0x1p-24);
+  const float gab = 0x1p-22f * sqrtf(static_cast<float>(a.dreal)) * a.inv_scale;
+  auto bound = [&](int r) -> float {
+    const float s = sqrtf(a.xnorm[idx[r]]) + sqrtf(cn[lab[r]]);
+    return gam * s * s + gab * s;
+  };
+  // pv = the ne-th largest lower bound est - b (ties by lower row), ne = the empty count
+  int ne0 = 0;
+  for (int c = 0; c < K; ++c) ne0 += (L.cnt[off + c] == 0);
+  float pv = __builtin_huge_valf();
+  int pi = -1;
+  for (int e = 0; e < ne0; ++e) {
+    float bv = -__builtin_huge_valf();
+    int bi = 0x7fffffff;
+    for (int r = tid; r < m; r += NT) {
+      const float lo = est[r] - bound(r);
+      if ((lo < pv || (lo == pv && r > pi)) && (lo > bv || (lo == bv && r < bi))) {
+        bv = lo;
+        bi = r;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o);
+      const int oi = __shfl_xor(bi, o);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      L.red_v[wave] = bv;
+      L.red_i[wave] = bi;
+    }
+    __syncthreads();
+    double gv = -__builtin_huge_val();
+    int gi = 0x7fffffff;
+    for (int w = 0; w < NW; ++w)
+      if (L.red_v[w] > gv || (L.red_v[w] == gv && L.red_i[w] < gi)) {
+        gv = L.red_v[w];
+        gi = L.red_i[w];
+      }
+    __syncthreads();
+    pv = static_cast<float>(gv);
+    pi = gi;
+  }
+  if (ne0 == 0 || a.reloc_full) pv = -__builtin_huge_valf();
+  // the candidates (est + b >= pv) get their exact squared distance to the centre they were
+  // assigned to: one wave per row, coalesced 16-B reads, f64 sum of the f32 squared differences
   float mymax = 0.f;
   for (int r = wave; r < m; r += NW) {
+    if (!(est[r] + bound(r) >= pv)) {
+      if (lane == 0) dist[r] = -2.f;
+      continue;
+    }
     const float4* x = reinterpret_cast<const float4*>(a.X + static_cast<size_t>(idx[r]) * dpad);
     const float4* c = reinterpret_cast<const float4*>(cold + static_cast<size_t>(lab[r]) * dpad);
     double acc = 0.0;
@@ -1122,7 +1187,8 @@ __device__ void post_body(const WArgs& a, PS& L, bool init) {
         const WProb& q = S.pr[p];
         relocate(a, L, idx, p, R.cen + (static_cast<size_t>(1 - q.ccur) * Cn + q.cenoff) * dpad,
                  R.cen + (static_cast<size_t>(q.ccur) * Cn + q.cenoff) * dpad,
-                 R.glab + (static_cast<size_t>(p) * 2 + q.lcur) * a.lsm, R.rdist, tid);
+                 R.glab + (static_cast<size_t>(p) * 2 + q.lcur) * a.lsm,
+                 R.dbuf + static_cast<size_t>(p) * a.ndb * a.lsm, R.cenn + q.cenoff, R.rdist, tid);
         __syncthreads();
       }
     }
@@ -1448,6 +1514,7 @@ extern "C" int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* 
   a.kpp_u = kpp_u;
   a.kpp_stride = kpp_stride;
   a.n_init = n_init;
+  a.reloc_full = std::getenv("CCMI_WIDE_RELOC_FULL") != nullptr;
   a.kpp_pos = kpp_pos;
   a.labels_out = labels_nh;
   a.ldl = ldl;

@@ -175,6 +175,26 @@ def test_wide_c4_shape():
     assert np.all(np.isfinite(inert))
 
 
+def test_wide_relocation_filter_is_exact(monkeypatch):
+    """Empty clusters in the wide engine: relocate() reads the exact distance only of rows whose
+    E-step distance, widened by its error bound, can reach the farthest ones.  With every row
+    read exactly (CCMI_WIDE_RELOC_FULL) the labels and inertia are identical; this data
+    relocates (6 times over 64 resamples x 9 problems)."""
+    from bench import make_expression_f32
+
+    X = make_expression_f32(1000, 2000, seed=1)
+    Ks, H, seed = [6, 9, 12], 64, 1
+    monkeypatch.delenv("CCMI_WIDE_RELOC_FULL", raising=False)
+    idx, labs, inert, nit, stats = run_gpu(X, Ks, H, 0.8, seed)
+    assert stats[3] > 0, "no relocation: the case no longer exercises the filter"
+    monkeypatch.setenv("CCMI_WIDE_RELOC_FULL", "1")
+    idx2, labs2, inert2, nit2, stats2 = run_gpu(X, Ks, H, 0.8, seed)
+    assert stats2[3] == stats[3]
+    np.testing.assert_array_equal(labs, labs2)
+    np.testing.assert_array_equal(inert, inert2)
+    np.testing.assert_array_equal(nit, nit2)
+
+
 def test_wide_expression_like():
     """BASELINE config 4's data family (bench.make_expression_f32: 5 groups, 500 informative
     features in N(0,1) noise) at a reduced size: labels agree with sklearn's on most problems
