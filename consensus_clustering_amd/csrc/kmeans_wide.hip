@@ -58,6 +58,9 @@ constexpr int KMAX = 127;
 constexpr int CTMAX = 8;
 constexpr int CNMAX = CTMAX * CWW;
 constexpr int RTB = 32;          // k-means++ cumsum block (rows)
+#ifndef KW_ALIGN
+#define KW_ALIGN 1               // align the problems' Lloyd phases (schedule)
+#endif
 
 enum { ST_SEED = 1, ST_RUN = 2, ST_FINAL = 3, ST_DONE = 4 };
 enum { IK_SEED0 = 0, IK_SEED = 1, IK_RUN = 2, IK_FINAL = 3 };
@@ -90,9 +93,10 @@ struct WProb {
 };
 
 struct WState {
-  int P, Cn, finished, pad;
+  int P, Cn, finished, round;  // round: P launches so far (the init is round 0)
   float tol;
-  int pad2[3];
+  int kmax;                    // largest K of the resample's problems
+  int pad2[2];
   WProb pr[PMAX];
 };
 
@@ -977,6 +981,13 @@ __device__ void schedule(const WArgs& a, PS& L, const int32_t* idx, const float*
   for (int p = 0; p < P; ++p) {
     WProb& q = S.pr[p];
     if (q.st != ST_SEED) continue;
+#if KW_ALIGN
+    // a problem starts seeding at round kmax - K, so that every problem's Lloyd iterations fall
+    // in the same rounds: the M launch streams all rows of a resample whenever any problem runs
+    // Lloyd, so rounds with Lloyd work are the ones to have fewest of (the order of problems
+    // changes no result)
+    if (q.c == 0 && S.round < S.kmax - static_cast<int>(q.K)) continue;
+#endif
     const int c = q.c, nt = (c == 0) ? 1 : q.ntr;
     int ct = 0;
     while (ct < nct && (L.tn[ct].nslots + nt > CWW || L.tn[ct].nitems + nt > IMW)) ++ct;
@@ -1017,6 +1028,9 @@ __device__ void post_body(const WArgs& a, PS& L, bool init) {
       S.P = a.P;
       S.Cn = a.Cn;
       S.finished = 0;
+      S.round = 0;
+      S.kmax = 0;
+      for (int p = 0; p < a.P; ++p) S.kmax = max(S.kmax, a.probs[4 * p]);
       int o = 0;
       for (int p = 0; p < a.P; ++p) {
         WProb& q = S.pr[p];
@@ -1050,6 +1064,7 @@ __device__ void post_body(const WArgs& a, PS& L, bool init) {
     }
     __syncthreads();
     if (S.finished) return;
+    if (tid == 0) S.round += 1;
     const int P = S.P, Cn = S.Cn;
     for (int ct = 0; ct < a.nct; ++ct) {
       const WTile* t = R.tiles + ct;
