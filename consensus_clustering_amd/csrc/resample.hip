@@ -138,12 +138,16 @@ __global__ __launch_bounds__(RS_NT) void resample_kernel(uint32_t seed, int n, i
 // steps, next-in-bucket, succ.
 constexpr int RSW_ARRAYS = 6;
 
+// The draws: 64 at a time, one per lane.  Within a block of 64 draws the step i_k of draw k lies
+// in [i - k, i] (at most k acceptances before it), so draw k is accepted for sure when
+// (v & mask) <= i - k and rejected for sure when (v & mask) > i.  When every lane is sure (and
+// neither the mask nor the end can change inside the block) the accepted lanes take steps
+// i - (accepted lanes before them) at once; otherwise (about 2000 / mask of the blocks, and the
+// last few thousand steps) lane 0 walks the block as numpy does.
 __global__ __launch_bounds__(RS_NT) void rsw_draw_kernel(uint32_t seed, int n, int h_begin, size_t stride,
                                                         uint32_t* J) {
   __shared__ uint32_t mt[MT_N], nw[MT_N];
   __shared__ __attribute__((aligned(16))) uint32_t draws[MT_N];
-  __shared__ uint32_t stage[MT_N];
-  __shared__ int st_i, st_c;
   const int lane = threadIdx.x;
   const int h = h_begin + blockIdx.x;
   uint32_t* Jh = J + static_cast<size_t>(blockIdx.x) * stride;
@@ -154,35 +158,39 @@ __global__ __launch_bounds__(RS_NT) void rsw_draw_kernel(uint32_t seed, int n, i
       x = 1812433253u * (x ^ (x >> 30)) + static_cast<uint32_t>(i);
       mt[i] = x;
     }
-    st_i = n - 1;
     Jh[0] = 0;
   }
   __syncthreads();
-  while (st_i >= 1) {  // wave-uniform
+  int i = n - 1;  // wave-uniform
+  uint32_t mask = interval_mask(static_cast<uint32_t>(i > 0 ? i : 0));
+  while (i >= 1) {
     mt_block(mt, nw, draws, lane);
-    const int i0 = st_i;
-    if (lane == 0) {
-      int i = i0, c = 0;
-      uint32_t mask = interval_mask(static_cast<uint32_t>(i));
-      for (int p = 0; p < MT_N && i >= 1; p += 4) {
-        const uint4 d4 = *reinterpret_cast<const uint4*>(draws + p);
-        const uint32_t dv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (i < 1) break;
-          const uint32_t v = dv[u] & mask;
-          if (v > static_cast<uint32_t>(i)) continue;  // rejected
-          stage[c++] = v;
-          --i;
-          if (static_cast<uint32_t>(i) <= (mask >> 1)) mask >>= 1;
+    for (int p = 0; p < MT_N && i >= 1; p += RS_NT) {
+      const int nb = min(RS_NT, MT_N - p);
+      const bool have = lane < nb;
+      const uint32_t v = have ? (draws[p + lane] & mask) : 0xFFFFFFFFu;
+      const bool acc = have && static_cast<int64_t>(v) <= static_cast<int64_t>(i) - lane;
+      const bool rej = !have || v > static_cast<uint32_t>(i);
+      const bool steady = i - RS_NT > static_cast<int>(mask >> 1) && i - RS_NT >= 1;  // mask and end fixed
+      if (steady && __all(acc || rej)) {
+        const unsigned long long bal = __ballot(acc);
+        const int before = __popcll(bal & ((1ull << lane) - 1ull));
+        if (acc) Jh[i - before] = v;
+        i -= __popcll(bal);
+      } else {
+        if (lane == 0) {
+          for (int q = 0; q < nb && i >= 1; ++q) {
+            const uint32_t w = draws[p + q] & mask;
+            if (w > static_cast<uint32_t>(i)) continue;  // rejected
+            Jh[i] = w;
+            --i;
+            if (static_cast<uint32_t>(i) <= (mask >> 1)) mask >>= 1;  // mask = interval_mask(i)
+          }
         }
+        i = __shfl(i, 0);
+        mask = __shfl(mask, 0);
       }
-      st_i = i;
-      st_c = c;
     }
-    __syncthreads();
-    for (int e = lane; e < st_c; e += RS_NT) Jh[i0 - e] = stage[e];  // steps i0, i0 - 1, ...
-    __syncthreads();
   }
 }
 
@@ -198,30 +206,56 @@ __global__ void rsw_count_kernel(int n, int nh, size_t stride, const uint32_t* _
 }
 
 __global__ __launch_bounds__(256) void rsw_scan_kernel(int n, size_t stride, uint32_t* cnt, uint32_t* cur) {
-  __shared__ uint32_t part[256];
+  // coalesced chunks of 1024 counts (16 B per thread), a block scan per chunk, a running carry;
+  // the next chunk's loads are issued before this chunk's scan
+  __shared__ uint32_t wsum[4];
   uint32_t* c = cnt + static_cast<size_t>(blockIdx.x) * stride;
   uint32_t* u = cur + static_cast<size_t>(blockIdx.x) * stride;
-  const int t = threadIdx.x;
-  const int per = (n + 255) / 256, b0 = t * per, b1 = min(n, b0 + per);
-  uint32_t s = 0;
-  for (int p = b0; p < b1; ++p) s += c[p];
-  part[t] = s;
-  __syncthreads();
-  if (t == 0) {
-    uint32_t run = 0;
-    for (int k = 0; k < 256; ++k) {
-      const uint32_t v = part[k];
-      part[k] = run;
-      run += v;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  auto load = [&](int base) -> uint4 {
+    const int i = base + 4 * t;
+    if (i + 3 < n) return *reinterpret_cast<const uint4*>(c + i);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (i < n) v.x = c[i];
+    if (i + 1 < n) v.y = c[i + 1];
+    if (i + 2 < n) v.z = c[i + 2];
+    return v;
+  };
+  uint32_t carry = 0;
+  uint4 v = load(0);
+  for (int base = 0; base < n; base += 1024) {
+    const uint4 vn = load(base + 1024 < n ? base + 1024 : base);
+    const uint32_t s = v.x + v.y + v.z + v.w;
+    uint32_t inc = s;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
     }
-  }
-  __syncthreads();
-  uint32_t run = part[t];
-  for (int p = b0; p < b1; ++p) {
-    const uint32_t v = c[p];
-    c[p] = run;  // exclusive offset
-    u[p] = 0;
-    run += v;
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t wpre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      wpre += (k < w) ? wsum[k] : 0u;
+      tot += wsum[k];
+    }
+    const uint32_t e0 = carry + wpre + inc - s;  // exclusive offset of this thread's first count
+    const int i = base + 4 * t;
+    const uint32_t o[4] = {e0, e0 + v.x, e0 + v.x + v.y, e0 + v.x + v.y + v.z};
+    if (i + 3 < n) {
+      *reinterpret_cast<uint4*>(c + i) = make_uint4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<uint4*>(u + i) = make_uint4(0, 0, 0, 0);
+    } else {
+      for (int k = 0; k < 4; ++k)
+        if (i + k < n) {
+          c[i + k] = o[k];
+          u[i + k] = 0;
+        }
+    }
+    carry += tot;
+    v = vn;
+    __syncthreads();  // wsum is rewritten by the next chunk
   }
 }
 

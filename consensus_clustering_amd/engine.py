@@ -86,8 +86,9 @@ def resample_indices(seed: int, n: int, m: int, h_begin: int, h_end: int, n_thre
     return out
 
 
-# workspace cap of the swap-partner resampling (resamples run in batches that fit)
-RESAMPLE_WIDE_WS = 1 << 30
+# workspace cap of the swap-partner resampling (resamples run in batches that fit; 4 GiB holds
+# every resample of C5 in one batch, one workgroup per resample across the whole GPU)
+RESAMPLE_WIDE_WS = 4 << 30
 
 
 def resample_indices_device(seed: int, n: int, m: int, h_begin: int, h_end: int, device,
