@@ -827,11 +827,19 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
     // block of 16 elements (all reads of a pass in flight together, then the counter adds).
     const bool interior = btab && !diag && (bj + 1) * T <= n && !full_out;
     if (interior && form == BT_TRI) {
+      // the next block's two co-sampling loads are issued before this block's table reads and
+      // counter adds (one block ahead: each block waited on its own HBM round trip)
+      uint4 n0 = it4[0], n1 = it4[1];
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int nj = 0; nj < 2; ++nj) {
-          const uint4 q0 = it4[(mi * 2 + nj) * 2], q1 = it4[(mi * 2 + nj) * 2 + 1];
+          const int blk = mi * 2 + nj;
+          const uint4 q0 = n0, q1 = n1;
+          if (blk < 7) {
+            n0 = it4[(blk + 1) * 2];
+            n1 = it4[(blk + 1) * 2 + 1];
+          }
           const uint32_t iw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
           uint32_t bb[16];
 #pragma unroll
@@ -845,11 +853,17 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           for (int v = 0; v < 16; ++v) atomicAdd(&hist[bb[v] * NT + tid], 1u);
         }
     } else if (interior && form == BT_PAIR) {
+      uint4 n0 = it4[0], n1 = it4[1];  // one block ahead, as above
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int nj = 0; nj < 2; ++nj) {
-          const uint4 q0 = it4[(mi * 2 + nj) * 2], q1 = it4[(mi * 2 + nj) * 2 + 1];
+          const int blk = mi * 2 + nj;
+          const uint4 q0 = n0, q1 = n1;
+          if (blk < 7) {
+            n0 = it4[(blk + 1) * 2];
+            n1 = it4[(blk + 1) * 2 + 1];
+          }
           const uint32_t iw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
           uint32_t ival[16];
           float rc[16];
@@ -878,11 +892,17 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
           }
         }
     } else if (interior) {
+      uint4 n0 = it4[0], n1 = it4[1];  // one block ahead, as above
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int nj = 0; nj < 2; ++nj) {
-          const uint4 q0 = it4[(mi * 2 + nj) * 2], q1 = it4[(mi * 2 + nj) * 2 + 1];
+          const int blk = mi * 2 + nj;
+          const uint4 q0 = n0, q1 = n1;
+          if (blk < 7) {
+            n0 = it4[(blk + 1) * 2];
+            n1 = it4[(blk + 1) * 2 + 1];
+          }
           const uint32_t iw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
           // table_bin_r for the block's 16 elements in three batched LDS passes (reciprocals,
           // then both thresholds, then the counter adds): one element at a time, every
