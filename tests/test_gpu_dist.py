@@ -1,6 +1,6 @@
 """The multi-rank product path: ConsensusClustering.fit under a 2-rank process group (gloo,
 both ranks on cuda:0) must give exactly the 1-rank fit — sharded resamples (k-means), the
-0xFF MIN-merge of the label matrix, the row-band sharded triangle tiles (I, M, histogram),
+all-gather of each rank's label columns, the row-band sharded triangle tiles (I, M, histogram),
 the SUM of the bin counts and, with keep_matrices, the band SUMs of the full I and M.
 Reference: the behaviour this replaces is CC.py:185-195 (joblib fan-out over resamples with
 an in-place shared M), which loses updates; here every count is an integer sum."""
