@@ -80,7 +80,7 @@ class ConsensusClustering:
         *,
         keep_matrices='auto',
         device=None,
-        workspace_budget=8 << 30,
+        workspace_budget=40 << 30,
         precision='auto',
         resampling='auto',
     ):

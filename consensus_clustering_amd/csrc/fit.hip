@@ -128,7 +128,7 @@ int choose_subsets(int nh, int n_groups, int cus) {
   return best;
 }
 
-int default_seedmax(int m) { return std::max(2, std::min(12, 1000000 / std::max(m, 1))); }
+int default_seedmax(int m) { return std::max(2, std::min(24, 4000000 / std::max(m, 1))); }  // kmeans.py default_seedmax
 
 int device_cus() {
   int dev = 0, cus = 0;

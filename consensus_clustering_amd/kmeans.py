@@ -90,12 +90,14 @@ def choose_subsets(nh: int, n_groups: int, cus: int) -> int:
 
 
 def default_seedmax(m: int) -> int:
-    """Problems of a unit that may seed (k-means++) concurrently.  Each seeding problem streams
-    closest-distance columns of m rows through HBM every sweep, so the cap shrinks with m.
-    Measured (k-means launch): C3 m = 40k: 6 / 8 / 10 / 12 / 14 / 16 / 20 -> 2692 / 2576 /
-    2530 / 2512 / 2517 / 2542 / 2555 ms; C5 m = 160k: 6 -> 464 ms, 8 -> 876 ms, 10 -> 898 ms;
-    C2 m = 8k: flat (130-132 ms for 10..32)."""
-    return max(2, min(12, 1_000_000 // max(int(m), 1)))
+    """Problems of a unit that may seed (k-means++) concurrently.  Each seeding problem keeps
+    closest-distance columns of m rows in the workspace (7 x m f32 per slot), so the cap shrinks
+    with m (<= ~110 MB of columns per workgroup).  Measured (k-means launch, round 3, with the
+    workspace budget not binding): C3 m = 40k: 12 / 16 / 20 / 24 / 32 -> 1679 / 1670 / 1656 /
+    1645 / 1647 ms; C5 m = 160k: 6 / 8 / 12 / 16 / 20 / 24 / 32 -> 281 / 283 / 276 / 276 / 275 /
+    273 / 273 ms; C2 m = 8k: 12 / 20 / 32 -> 88.2 / 87.5 / 87.0 ms.  (Round 1 measured 6 best
+    at C5: there the larger caps passed the 8 GB budget and halved the grid.)"""
+    return max(2, min(24, 4_000_000 // max(int(m), 1)))
 
 
 def kpp_tables(Ks, n_init: int, seed: int, m: int, weight_dtype=np.float32):
@@ -152,7 +154,7 @@ class BatchedKMeans:
     """All (h, K, init) k-means problems of a consensus fit, on one device."""
 
     def __init__(self, Ks, n_init=3, max_iter=300, tol=1e-4, random_state=0,
-                 workspace_budget=8 << 30, seedmax=None, wide_budget=96 << 30):
+                 workspace_budget=40 << 30, seedmax=None, wide_budget=96 << 30):
         self.Ks = [int(k) for k in Ks]
         self.n_init = int(n_init)
         self.max_iter = int(max_iter)
@@ -193,7 +195,8 @@ class BatchedKMeans:
         lib = _lib.load()
         per = lambda g: lib.cc_kmeans_workspace_bytes(m, Xd.shape[1], u_h.ctypes.data, nU, seedmax, g)
         grid = min(cus, nh * nU)
-        while grid > 1 and per(grid) > self.workspace_budget:
+        budget = min(self.workspace_budget, int(0.5 * torch.cuda.mem_get_info(dev)[0]))
+        while grid > 1 and per(grid) > budget:
             grid //= 2
         ws = workspace(dev, per(grid))
         ldl = labels_nh.stride(1)
