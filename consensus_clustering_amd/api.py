@@ -21,8 +21,10 @@ What runs where (``fit``):
 Deliberate differences, all documented in DESIGN.md: the constructor does not delete
 files in ``memmap_folder`` (CC.py:83-86); the n x n matrices are materialised only when
 ``keep_matrices`` (default: n <= 20000) since the reference's O(n^2)-per-K retention is
-infeasible at n = 50k; parallel arguments (n_jobs, parallelization_method) are accepted
-and ignored (the reference's threads/processes paths race).
+infeasible at n = 50k; n_jobs / parallelization_method parallelise only the host fits of a
+foreign clusterer (``host_fit_predict``: joblib threads or processes as CC.py:185-195, with
+labels returned instead of added into a shared Mij, so nothing races; the default KMeans runs on
+the GPU whatever n_jobs says).
 Additions: ``cdf_area_``, ``delta_k_``, ``pac_area_``, ``best_k_`` and ``predict``.
 """
 from __future__ import annotations
@@ -104,8 +106,8 @@ class ConsensusClustering:
         self.device = device
         self.workspace_budget = workspace_budget
         # k-means arithmetic: 'f64' = float64 like sklearn on float64 input (cc_kmeans_f64),
-        # 'fast' = the float32-class f16 hi/lo MFMA engine; 'auto' = f64 for float64 input while
-        # the float64 engine's work is small (F64_AUTO_MAX_WORK), else fast with a warning
+        # 'fast' = the float32-class f16 hi/lo MFMA engine; 'auto' = f64 for float64 input, fast
+        # for float32 (sklearn's own choice of arithmetic follows X's dtype)
         self.precision = precision
         # where the resample indices are drawn: 'device' (cc_resample_device for n <= 65536,
         # cc_resample_device_wide above), 'host' (native threads, then uploaded), 'auto' =
@@ -216,20 +218,10 @@ class ConsensusClustering:
         self.backend_ = 'gpu-kmeans' if km is not None else 'host-clusterer'
         precision = self.precision
         if precision == 'auto':
-            precision = 'fast'
-            if wdtype == np.float64 and km is not None:
-                # float64 input: the reference's clusterer runs in float64 (CC.py:282), which
-                # cc_kmeans_f64 reproduces, but at ~40x the fast engine's time (one workgroup
-                # per (resample, K); 4.2 s per C3 resample against 0.11 s,
-                # profiles/r03/f64_vs_fast_c3_H4.txt): take it only while it stays small
-                work = float(H) * m * X.shape[1] * sum(Ks) * km["n_init"]
-                if work <= self.F64_AUTO_MAX_WORK:
-                    precision = 'f64'
-                else:
-                    warnings.warn(
-                        f"float64 input: the float64 k-means would take ~{work * 1.3e-9:.0f} s here; "
-                        "using the float32-class engine (precision='fast'); pass precision='f64' "
-                        "to force sklearn's float64 arithmetic")
+            # the reference's clusterer computes in X's dtype (CC.py:282): float64 input keeps
+            # sklearn's float64 arithmetic (cc_kmeans_f64) whatever the size; the float32-class
+            # engine is opt-in for it (precision='fast')
+            precision = 'f64' if (wdtype == np.float64 and km is not None) else 'fast'
         if precision not in ('f64', 'fast'):
             raise ValueError("precision must be 'auto', 'f64' or 'fast'")
         self.precision_ = precision if km is not None else None
@@ -260,9 +252,8 @@ class ConsensusClustering:
             for k, K in enumerate(Ks):
                 self._K = K
                 self._set_clusterer_K()
-                lab = np.empty((h1 - h0, m), dtype=np.int32)
-                for h in range(h0, h1):
-                    lab[h - h0] = np.asarray(self.clusterer.fit_predict(X[idx[h]]))
+                lab = host_fit_predict(self.clusterer, X, idx[h0:h1], self.n_jobs,
+                                       self.parallelization_method)
                 if lab.size and (lab.min() < 0 or lab.max() >= K):
                     raise ValueError(f"clusterer labels must lie in [0, {K})")
                 engine.scatter_labels(idx_d[h0:h1].contiguous(), torch.from_numpy(lab).to(dev), n,
@@ -389,10 +380,6 @@ class ConsensusClustering:
             out[K] = path
         return out
 
-    # precision='auto' on float64 input: the float64 k-means while H m d sum(K) n_init stays at
-    # or below this (about 1 s of cc_kmeans_f64 at the measured ~1.3 ns per unit; C1 is 1.1e7)
-    F64_AUTO_MAX_WORK = 7.5e8
-
     # largest n for predict() with linkage='single' (a host linkage over n x n float64 distances);
     # 'average', 'complete' and 'weighted' run on the device for any n that fits in HBM
     PREDICT_MAX_N = 20000
@@ -419,6 +406,19 @@ class ConsensusClustering:
         K = self.best_k_ if K is None else K
         n = self._N
         link = self.agg_clustering_linkage
+        # sklearn's checks (AgglomerativeClustering's parameter validation, check_array's minimum
+        # of 2 samples, _hc_cut), raised before any device work
+        if isinstance(K, bool) or not isinstance(K, (int, np.integer)) or K < 1:
+            raise ValueError("The 'n_clusters' parameter of AgglomerativeClustering must be an int "
+                             f"in the range [1, inf) or None. Got {K!r} instead.")
+        if n < 2:
+            raise ValueError(f"Found array with {n} sample(s) (shape=({n}, {n})) while a minimum of "
+                             "2 is required by AgglomerativeClustering.")
+        if K > n:
+            raise ValueError("Cannot extract more clusters than samples: "
+                             f"{K} clusters were given for a tree with {n} leaves.")
+        if K not in self.cdf_at_K_data:
+            raise KeyError(f"K = {K} is not in K_range of the fit")
         if link == 'ward':
             raise ValueError("ward linkage needs the euclidean metric; the reference's manhattan "
                              "consensus linkage supports 'average', 'complete' and 'single'")
@@ -482,6 +482,56 @@ class ConsensusClustering:
         if show:
             plt.show()
         return ax
+
+
+def _clone(clusterer):
+    """An independent copy of a plugin clusterer with the same parameters: sklearn's ``clone``
+    for estimators (get_params), else a deep copy."""
+    if hasattr(clusterer, 'get_params'):
+        try:
+            from sklearn.base import clone
+
+            return clone(clusterer)
+        except Exception:  # not a clonable sklearn estimator
+            pass
+    import copy
+
+    return copy.deepcopy(clusterer)
+
+
+def _fit_predict_one(clusterer, Xs):
+    return np.asarray(clusterer.fit_predict(Xs))
+
+
+def host_fit_predict(clusterer, X, idx, n_jobs=1, parallelization_method='multithreading'):
+    """int32 labels [len(idx), m] of ``clusterer.fit_predict(X[idx[h]])`` for every resample h
+    (CC.py:282), the hybrid path's host stage for a clusterer the GPU k-means does not replace.
+
+    n_jobs == 1: one call after the other on the clusterer itself (CC.py:180-183).  Otherwise the
+    resamples fan out over joblib workers as CC.py:185-195 does: threads for
+    'multithreading', processes for 'multiprocessing' (n_jobs=-1: all cores).  Labels are
+    RETURNED, not accumulated into a shared matrix, so the workers cannot race (the reference adds
+    into one shared Mij from every worker); under threads each task fits its own copy of the
+    clusterer (the reference shares one, whose fit_predict can return another thread's labels).
+    The labels do not depend on n_jobs."""
+    H = len(idx)
+    if H == 0:
+        return np.empty((0, 0), dtype=np.int32)
+    if n_jobs == 1:
+        return np.stack([_fit_predict_one(clusterer, X[i]) for i in idx]).astype(np.int32)
+    if parallelization_method == 'multithreading':
+        prefer = 'threads'
+        make = _clone
+    elif parallelization_method == 'multiprocessing':
+        prefer = 'processes'
+        make = lambda c: c  # noqa: E731  (pickled per task by joblib)
+    else:
+        raise RuntimeError(f'unknown parallelization method: {parallelization_method}')
+    from joblib import Parallel, delayed
+
+    out = Parallel(n_jobs=n_jobs, prefer=prefer)(
+        delayed(_fit_predict_one)(make(clusterer), X[i]) for i in idx)
+    return np.stack(out).astype(np.int32)
 
 
 def _prepare(X, dev):

@@ -7,8 +7,9 @@ independent and every count is an integer sum, so a fit shards exactly:
 * resamples   rank r runs k-means for h in ``shard(H, r, W)`` (no communication);
 * labels      each rank packs its own resample columns [h0, h1) of the sample-major
               [nK, n, Hpad] label matrix into a contiguous [nK, n, hw] block
-              (hw = ceil(H / W)), the blocks are ALL-GATHERED (RCCL over xGMI on the GPU;
-              gloo in the CPU tests) and every block is placed back at its columns.  Per GPU
+              (hw = ceil(H / W)), the blocks are ALL-GATHERED into one flat buffer
+              (``all_gather_into_tensor``: RCCL over xGMI on the GPU, gloo in the CPU tests;
+              the same call either way) and every block is placed back at its columns.  Per GPU
               that moves (W-1)/W of nK n H bytes; a MIN all-reduce of the whole matrix (the
               round-2 exchange) moved 2 (W-1)/W of nK n Hpad;
 * triangle    rank r owns tiles ``shard(num_tiles, r, W)`` of the upper-triangle
@@ -19,9 +20,10 @@ independent and every count is an integer sum, so a fit shards exactly:
 
 Bit-exact for every W: integer counts, order-free reductions.
 
-The exchanges use the default process group.  With the ``gloo`` backend (CPU tests, and
-the single-GPU multi-process tests that put several ranks on one device) device tensors
-are reduced through a host copy; with ``nccl`` (RCCL) they are reduced in place.
+The exchanges use the default process group and the same collective calls on every backend.
+The only backend-dependent step is ``_host_staged``: with ``gloo`` (the CPU tests, and the
+single-GPU multi-process tests that put several ranks on one device) a device tensor is
+exchanged through a host copy; with ``nccl`` (RCCL) in place.
 """
 from __future__ import annotations
 
@@ -47,16 +49,32 @@ def shard(total: int, rank: int, world_size: int) -> tuple:
     return begin, begin + base + (1 if rank < rem else 0)
 
 
+def _host_staged(t: torch.Tensor) -> bool:
+    """gloo reduces host tensors only: a device tensor goes through a host copy.  This is the one
+    place the backend matters; the collectives themselves are the same calls on RCCL and gloo."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
 def _all_reduce(t: torch.Tensor, op) -> torch.Tensor:
     if not (_live() and dist.get_world_size() > 1):
         return t
-    if t.is_cuda and dist.get_backend() == "gloo":
-        h = t.cpu()
-        dist.all_reduce(h, op=op)
-        t.copy_(h)
-    else:
-        dist.all_reduce(t, op=op)
+    buf = t.cpu() if _host_staged(t) else t
+    dist.all_reduce(buf, op=op)
+    if buf is not t:
+        t.copy_(buf)
     return t
+
+
+def all_gather_flat(t: torch.Tensor) -> torch.Tensor:
+    """Every rank's contiguous ``t`` (same shape on all ranks) gathered in rank order into one
+    [W, *t.shape] tensor on t's device: ``all_gather_into_tensor`` into a flat W * numel buffer
+    (RCCL over xGMI on the GPU; gloo, with a host copy, in the CPU tests)."""
+    W = dist.get_world_size()
+    src = t.cpu() if _host_staged(t) else t
+    out = torch.empty(W * src.numel(), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src.reshape(-1))
+    out = out.view((W,) + tuple(t.shape))
+    return out.to(t.device) if src is not t else out
 
 
 def _copy_columns(src, col_src, dst, col_dst, width):
@@ -83,20 +101,12 @@ def merge_labels(labels: torch.Tensor, H: int) -> torch.Tensor:
     h0, h1 = shard(H, rank, W)
     stage = torch.full(lead + (hw,), 0xFF, dtype=torch.uint8, device=labels.device)
     _copy_columns(labels, h0, stage, 0, h1 - h0)
-    if labels.is_cuda and dist.get_backend() != "gloo":
-        gathered = torch.empty((W,) + lead + (hw,), dtype=torch.uint8, device=labels.device)
-        dist.all_gather_into_tensor(gathered, stage)
-        blocks = list(gathered.unbind(0))
-    else:
-        host = stage.cpu()
-        parts = [torch.empty_like(host) for _ in range(W)]
-        dist.all_gather(parts, host)
-        blocks = [p.to(labels.device) for p in parts]
-    for r, blk in enumerate(blocks):
+    blocks = all_gather_flat(stage)  # [W, nK, n, hw], rank r's block at [r]
+    for r in range(W):
         if r == rank:
             continue
         a, b = shard(H, r, W)
-        _copy_columns(blk.contiguous(), 0, labels, a, b - a)
+        _copy_columns(blocks[r], 0, labels, a, b - a)
     return labels
 
 

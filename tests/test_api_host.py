@@ -39,3 +39,25 @@ def test_plot_cdf_opens_and_shows_a_figure(monkeypatch):
     fig, ax2 = plt.subplots()
     assert cc._plot_cdf(ax=ax2) is ax2 and shown == [True]  # embedding: no show
     plt.close("all")
+
+
+@pytest.mark.parametrize("method,n_jobs", [("multithreading", 4), ("multiprocessing", 2)])
+def test_host_fit_predict_parallel_equals_serial(method, n_jobs):
+    """The hybrid path's host fits (a foreign clusterer, CC.py:282) fanned out over joblib threads
+    or processes as CC.py:185-195 does: the labels equal the serial loop's, in resample order."""
+    from sklearn.mixture import GaussianMixture
+    from threadpoolctl import threadpool_limits
+
+    from consensus_clustering_amd.api import host_fit_predict
+    from tests.conftest import load_fixture
+
+    f = load_fixture("c1_corr_pt_gmm")
+    X, idx = f["X"], f["indices"][:8]
+    gmm = GaussianMixture(n_components=5, n_init=3, random_state=23)  # after set_params (CC.py:212)
+    with threadpool_limits(1):
+        serial = host_fit_predict(gmm, X, idx)
+        par = host_fit_predict(gmm, X, idx, n_jobs=n_jobs, parallelization_method=method)
+    np.testing.assert_array_equal(par, serial)
+    np.testing.assert_array_equal(serial, f["labels"][0, :8])
+    with pytest.raises(RuntimeError, match="unknown parallelization method"):
+        host_fit_predict(gmm, X, idx, n_jobs=2, parallelization_method="mpi")

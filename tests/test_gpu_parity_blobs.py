@@ -1,0 +1,181 @@
+"""End-to-end parity at a realistic size against the REFERENCE's own run.
+
+Fixtures: tests/golden/make_parity_blobs.py ran consensus_clustering_parallelised.py itself on
+seeded blobs n = 3000, d = 32, k_true = 6, K = 2..12, H = 60 (CC.py:92-136), once with float64
+X and once with float32 X, recording every label vector its clusterer returned.  The reference's
+M of every K is rebuilt here from those labels by the bit-exact co-association and checked
+against the SHA-256 of the reference's own mij before it is used, so the reference's C is known
+exactly.
+
+* float64 input (precision='auto' -> cc_kmeans_f64, sklearn's float64 arithmetic): every label,
+  every K's mij and cij, hist, cdf and PAC identical to the reference, the same best K.
+* float32 input (the f16 hi/lo MFMA engine: sklearn float32's accuracy class, not its rounding):
+  identical M, C, hist, cdf and PAC for K <= k_true, the same best K, and for K > k_true |dPAC|
+  and max |dC| reported and bounded.  sklearn's float32 fit is not reproducible there even by
+  sklearn (tests/test_parity_fixtures.py, tools/sklearn_self_parity.py).
+* the C2 shape (n = 10 000, d = 64, k_true = 6, K = 2..15) at H = 50: sklearn's float32 labels
+  (computed here, 1 BLAS thread per fit) fed through the same co-association give the
+  reference's PAC per K; the engine's own fit is compared with it the same way.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import digest, load_fixture
+
+pytestmark = pytest.mark.gpu
+
+# float32 input, K > k_true: bounds on the engine's distance from the reference's result
+F32_MAX_DPAC = 0.02
+F32_MAX_DC = 0.25
+
+
+def _fit(pf, **kw):
+    from consensus_clustering_amd import ConsensusClustering
+
+    meta = pf["meta"]
+    cc = ConsensusClustering(K_range=[int(k) for k in pf["K_range"]], n_iterations=meta["H"],
+                             subsampling=meta["subsampling"], random_state=meta["random_state"],
+                             plot_cdf=False, **kw)
+    return cc.fit(pf["X"])
+
+
+def _reference_counts(idx_hm, labels_khm, Ks, n, H, dev):
+    """int32 M per K and I (device) from labels in resample order (the reference's fixture or a
+    host clusterer), through the product co-association (cc_scatter_labels, cc_cosample,
+    cc_coassoc)."""
+    from consensus_clustering_amd import engine
+
+    Hpad = engine.pad_h(H)
+    idx_d = torch.from_numpy(np.ascontiguousarray(idx_hm, dtype=np.int32)).to(dev)
+    L = engine.new_label_matrix(len(Ks), n, Hpad, dev)
+    for j in range(len(Ks)):
+        lab = torch.from_numpy(np.ascontiguousarray(labels_khm[j], dtype=np.int32)).to(dev)
+        engine.scatter_labels(idx_d, lab, n, L[j])
+    nt = engine.num_tiles(n)
+    I_tiles, I_full = engine.cosample(L[0], n, Hpad, 0, nt, want_full=True)
+    edges = engine.edges_device(dev)
+    Ms, counts = [], []
+    for j, K in enumerate(Ks):
+        c = torch.zeros(20, dtype=torch.int64, device=dev)
+        M = torch.zeros((n, n), dtype=torch.int32, device=dev)
+        engine.coassoc(L[j], n, Hpad, K, 0, nt, I_tiles, edges, c, M)
+        Ms.append(M)
+        counts.append(c.cpu().numpy())
+    return Ms, I_full, counts
+
+
+def _pac_of_counts(c, n):
+    from consensus_clustering_amd import post
+
+    return post.cdf_from_counts(post.pair_counts_to_hist_counts(c, n))[3]
+
+
+def _label_agreement(cc, pf):
+    """Problems (K, h) whose engine labels equal the recorded ones, of all."""
+    L = cc.labels_
+    idx = pf["indices"]
+    same = 0
+    for j in range(len(pf["K_range"])):
+        col = L[j].cpu().numpy()
+        for h in range(idx.shape[0]):
+            same += np.array_equal(col[idx[h], h].astype(np.int64), pf["labels"][j, h])
+    return same, len(pf["K_range"]) * idx.shape[0]
+
+
+def test_float64_input_identical_to_reference():
+    pf = load_fixture("parity_blobs_n3000_f64")
+    meta = pf["meta"]
+    cc = _fit(pf)
+    assert cc.precision_ == "f64"
+    Ks = [int(k) for k in pf["K_range"]]
+    same, total = _label_agreement(cc, pf)
+    print(f"float64 input: {same}/{total} (K, h) label vectors identical to the reference's")
+    assert digest(cc.cdf_at_K_data[Ks[0]]["iij"]) == meta["iij_sha256"]
+    for j, K in enumerate(Ks):
+        d = cc.cdf_at_K_data[K]
+        assert digest(d["mij"]) == meta["mij_sha256"][str(K)], K
+        assert digest(d["cij"]) == meta["cij_sha256"][str(K)], K
+        np.testing.assert_array_equal(d["hist"], pf["hist"][j])
+        np.testing.assert_array_equal(d["cdf"], pf["cdf"][j])
+        assert d["pac_area"] == pf["pac_area"][j], K
+    assert same == total
+    assert cc.best_k_ == meta["best_k"]
+
+
+def test_float32_input_against_reference():
+    from consensus_clustering_amd import engine
+
+    pf = load_fixture("parity_blobs_n3000_f32")
+    meta = pf["meta"]
+    n, H, kt = pf["X"].shape[0], meta["H"], meta["k_true"]
+    cc = _fit(pf)
+    assert cc.precision_ == "fast"
+    Ks = [int(k) for k in pf["K_range"]]
+    dev = cc.labels_.device
+    Ms, I, counts = _reference_counts(pf["indices"], pf["labels"], Ks, n, H, dev)
+    assert digest(I.cpu().numpy().astype(np.uint8)) == meta["iij_sha256"]
+    same, total = _label_agreement(cc, pf)
+    report = []
+    for j, K in enumerate(Ks):
+        d = cc.cdf_at_K_data[K]
+        assert digest(Ms[j].cpu().numpy().astype(np.uint8)) == meta["mij_sha256"][str(K)], K
+        C_ref = engine.consensus(Ms[j], I)
+        C = torch.from_numpy(d["cij"]).to(dev)
+        dC = float((C - C_ref).abs().max())
+        dpac = abs(float(d["pac_area"]) - float(pf["pac_area"][j]))
+        report.append((K, round(dpac, 6), round(dC, 4)))
+        if K <= kt:
+            assert digest(d["mij"]) == meta["mij_sha256"][str(K)], K
+            assert digest(d["cij"]) == meta["cij_sha256"][str(K)], K
+            np.testing.assert_array_equal(d["hist"], pf["hist"][j])
+            np.testing.assert_array_equal(d["cdf"], pf["cdf"][j])
+            assert d["pac_area"] == pf["pac_area"][j], K
+    print(f"float32 input: {same}/{total} (K, h) label vectors identical; (K, |dPAC|, max |dC|):",
+          report)
+    assert max(r[1] for r in report) <= F32_MAX_DPAC, report
+    assert max(r[2] for r in report) <= F32_MAX_DC, report
+    assert cc.best_k_ == meta["best_k"]
+
+
+def _sk_labels(X, idx, K, seed):
+    from oracle import cc_oracle as O
+
+    return np.stack([O.kmeans_labels(X[i], K, seed, n_init=3) for i in idx])
+
+
+def test_c2_shape_h50_sklearn_labels_through_coassoc():
+    """C2's shape at H = 50: sklearn's float32 labels for every (K, h) through the bit-exact
+    co-association give the reference's pair counts and PAC; the engine's fit is held to the same
+    bounds as above (identical counts for K <= k_true, bounded |dPAC| above, same best K)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from threadpoolctl import threadpool_limits
+
+    from bench import SEED, make_blobs_f32
+    from consensus_clustering_amd import ConsensusClustering, post
+
+    n, d, kt, H = 10000, 64, 6, 50
+    Ks = list(range(2, 16))
+    X = make_blobs_f32(n, d, kt, seed=SEED)
+    cc = ConsensusClustering(K_range=Ks, n_iterations=H, subsampling=0.8, random_state=SEED,
+                             plot_cdf=False, keep_matrices=False)
+    cc.fit(X)
+    idx = cc.resampling_indices_
+    dev = cc.labels_.device
+    # 700 single-thread sklearn fits on 16 host threads (sklearn's Lloyd releases the GIL)
+    # (the limit is process-wide, so it is set once around all the threads)
+    with threadpool_limits(1), ThreadPoolExecutor(16) as ex:
+        labs = list(ex.map(lambda K: _sk_labels(X, idx, K, SEED), Ks))
+    _, _, counts = _reference_counts(idx, labs, Ks, n, H, dev)
+    report = []
+    pac_ref = {}
+    for j, K in enumerate(Ks):
+        pac_ref[K] = float(_pac_of_counts(counts[j], n))
+        dpac = abs(float(cc.pac_area_[K]) - pac_ref[K])
+        report.append((K, round(dpac, 6)))
+        if K <= kt:
+            np.testing.assert_array_equal(cc.pair_counts_[K], counts[j], err_msg=f"K={K}")
+    print("C2 shape, H = 50: (K, |dPAC| vs sklearn labels):", report)
+    assert max(r[1] for r in report) <= F32_MAX_DPAC, report
+    assert cc.best_k_ == post.best_k(pac_ref)

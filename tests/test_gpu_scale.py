@@ -178,8 +178,7 @@ def test_c4_full_size():
     check_counts_sum(cfg, cc)
     check_labels(cfg, cc)
     check_tiles(cfg, cc, Ks_check=[2, 5, 12])
-    # the wide engine's known gap: at most one unexplained problem
-    sklearn_parity(X, cc.labels_, cc.resampling_indices_, cfg["Ks"], SEED, resamples=1, max_unexplained=1)
+    sklearn_parity(X, cc.labels_, cc.resampling_indices_, cfg["Ks"], SEED, resamples=1)
 
 
 def test_c3_full_size():
