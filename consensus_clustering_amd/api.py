@@ -380,10 +380,6 @@ class ConsensusClustering:
             out[K] = path
         return out
 
-    # largest n for predict() with linkage='single' (a host linkage over n x n float64 distances);
-    # 'average', 'complete' and 'weighted' run on the device for any n that fits in HBM
-    PREDICT_MAX_N = 20000
-
     def predict(self, K=None, distance='manhattan'):
         """Consensus labels for K (default ``best_k_``).
 
@@ -396,9 +392,10 @@ class ConsensusClustering:
         scipy's summation order (cc_manhattan, bit-identical to
         ``scipy.spatial.distance.pdist(C, 'cityblock')``), and for 'average', 'complete' and
         'weighted' linkage scipy's nn_chain (cc_linkage_nnchain), whose merges the host sorts,
-        relabels and cuts as scipy's linkage() and sklearn's ``_hc_cut`` do.  n is bounded by HBM
-        (C, then 8 n^2 bytes of distances: 20 GB at n = 50 000).  'single' linkage keeps the host
-        path (sklearn's own minimum-spanning-tree code), for n <= PREDICT_MAX_N.
+        relabels and cuts as scipy's linkage() and sklearn's ``_hc_cut`` do; for 'single' linkage
+        sklearn's own mst_linkage_core (Prim, cc_linkage_mst), sorted and labelled as sklearn's
+        linkage_tree does.  n is bounded by HBM (C, then 8 n^2 bytes of distances: 20 GB at
+        n = 50 000).
 
         distance='1-C' is an opt-in variant: the same linkage over 1 - C as a precomputed
         consensus distance.
@@ -424,29 +421,17 @@ class ConsensusClustering:
                              "consensus linkage supports 'average', 'complete' and 'single'")
         if distance not in ('manhattan', '1-C'):
             raise ValueError("distance must be 'manhattan' or '1-C'")
-        if link in engine.LINKAGE_METHODS:
+        if link in engine.LINKAGE_METHODS or link == 'single':
             C = self._consensus_device(K)
             if distance == 'manhattan':
                 D = engine.manhattan(C)
             else:
                 D = 1.0 - C.double()
             del C
-            Z = engine.linkage(D, link)
+            Z = engine.linkage_single(D) if link == 'single' else engine.linkage(D, link)
             del D
             return post.hc_cut(K, Z[:, :2].astype(np.int64), n)
-        from sklearn.cluster import AgglomerativeClustering
-
-        if n > self.PREDICT_MAX_N:
-            raise ValueError(f"predict(): n = {n} > PREDICT_MAX_N = {self.PREDICT_MAX_N} for linkage "
-                             f"'{link}' (host linkage over n^2 float64 distances)")
-        C = self.consensus_matrix(K)
-        if distance == 'manhattan':
-            D = engine.manhattan(torch.from_numpy(np.ascontiguousarray(C)).to(self.labels_.device))
-            D = D.cpu().numpy()
-        else:
-            D = 1.0 - C.astype(np.float64)
-        agg = AgglomerativeClustering(n_clusters=K, metric='precomputed', linkage=link)
-        return agg.fit_predict(D)
+        raise ValueError(f"unknown linkage {link!r}: 'average', 'complete', 'weighted' or 'single'")
 
     @property
     def resampling_indices_(self):

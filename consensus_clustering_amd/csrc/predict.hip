@@ -110,9 +110,21 @@ extern "C" int cc_manhattan(const float* C, int n, int d, double* D, void* strea
 // runs the whole chain (every step is a scan or an update over n entries; the full symmetric
 // n x n float64 matrix stays in HBM: 20 GB at n = 50k).  Z is written in merge order, unsorted;
 // the host sorts it by distance (stable) and relabels, as linkage() does after nn_chain.
+//
+// Round 4: the live set is a bitmask in LDS (n / 8 bytes), and every row pass issues its loads
+// in batches of NB per thread before any compare (branch-free: dead and diagonal entries read
+// as +inf), so a scan is a few HBM round trips instead of one per element and thread (8.3 s ->
+// see DESIGN.md K7 at n = 50k).
+//
+// Single linkage: sklearn's own path (linkage_tree -> _hierarchical_fast.mst_linkage_core, Prim's
+// MST-LINKAGE-CORE, for a non-precomputed metric such as the reference's 'manhattan'): from node 0,
+// each step folds the current node's row into the running minimum distance of every node not in
+// the tree (strict <) and takes the first node of the smallest, as mst_kernel does with D's rows
+// (the cityblock values of DistanceMetric64 are cc_manhattan's, same terms and order).
 namespace {
 
 constexpr int LT = 1024;  // threads of the linkage workgroup
+constexpr int NB = 8;     // loads per thread in flight per row pass
 
 __device__ __forceinline__ double lw_update(int method, double dxi, double dyi, int nx, int ny) {
 #pragma clang fp contract(off)  // scipy's products and sum rounded separately (no FMA)
@@ -150,24 +162,56 @@ __device__ __forceinline__ void block_argmin(double& v, int& i, double* rv, int*
     }
 }
 
+__device__ __forceinline__ bool live(const unsigned* mask, int i) { return (mask[i >> 5] >> (i & 31)) & 1u; }
+
+// First minimum over live i != x of row[i]: thread tid visits i = base + tid + LT u in increasing
+// order, NB loads in flight per batch.
+__device__ __forceinline__ void row_argmin(const double* row, int n, int x, const unsigned* mask, double& v,
+                                           int& bi) {
+  constexpr double INF = __builtin_huge_val();
+  const int tid = threadIdx.x;
+  v = INF;
+  bi = 0x7fffffff;
+  for (int base = 0; base < n; base += LT * NB) {
+    double d[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int i = base + tid + LT * u;
+      d[u] = i < n ? row[i] : INF;
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int i = base + tid + LT * u;
+      const bool ok = i < n && i != x && live(mask, i);
+      if (ok && d[u] < v) {
+        v = d[u];
+        bi = i;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(LT) void nnchain_kernel(double* __restrict__ D, int n, int method,
                                                      double* __restrict__ Z, int* __restrict__ size,
                                                      int* __restrict__ chain) {
+  extern __shared__ unsigned mask[];  // live clusters, one bit each
   __shared__ double rv[LT / 64];
   __shared__ int ri[LT / 64];
   const int tid = threadIdx.x;
   const size_t nn = static_cast<size_t>(n);
+  const int nw = (n + 31) >> 5;
   constexpr double INF = __builtin_huge_val();
   for (int i = tid; i < n; i += LT) size[i] = 1;
+  for (int w = tid; w < nw; w += LT) mask[w] = (w < nw - 1 || (n & 31) == 0) ? 0xFFFFFFFFu : ((1u << (n & 31)) - 1u);
   __syncthreads();
   int len = 0;  // uniform: every thread runs the same control flow
   for (int k = 0; k < n - 1; ++k) {
     if (len == 0) {  // the first live cluster
       double v = INF;
       int i0 = 0x7fffffff;
-      for (int i = tid; i < n; i += LT)
-        if (size[i] > 0) {
-          i0 = i;
+      for (int w = tid; w < nw; w += LT)
+        if (mask[w]) {
+          i0 = 32 * w + __builtin_ctz(mask[w]);
           v = 0.0;
           break;
         }
@@ -186,17 +230,9 @@ __global__ __launch_bounds__(LT) void nnchain_kernel(double* __restrict__ D, int
         y = chain[len - 2];
         cur = D[x * nn + y];
       }
-      const double* row = D + x * nn;
-      double v = INF;
-      int bi = 0x7fffffff;
-      for (int i = tid; i < n; i += LT) {
-        if (i == x || size[i] == 0) continue;
-        const double d = row[i];
-        if (d < v) {  // increasing i per thread: the first minimum
-          v = d;
-          bi = i;
-        }
-      }
+      double v;
+      int bi;
+      row_argmin(D + x * nn, n, x, mask, v, bi);
       block_argmin(v, bi, rv, ri);
       if (v < cur) {
         cur = v;
@@ -223,19 +259,94 @@ __global__ __launch_bounds__(LT) void nnchain_kernel(double* __restrict__ D, int
       Z[4 * static_cast<size_t>(k) + 3] = nx + ny;
       size[x] = 0;
       size[y] = nx + ny;
+      mask[x >> 5] &= ~(1u << (x & 31));
     }
     __syncthreads();
     const double* rx = D + x * nn;
     double* ry = D + y * nn;
-    for (int i = tid; i < n; i += LT) {
-      if (i == y || size[i] == 0) continue;
-      const double nd = lw_update(method, rx[i], ry[i], nx, ny);
-      ry[i] = nd;
-      D[i * nn + y] = nd;
+    for (int base = 0; base < n; base += LT * NB) {
+      double dx[NB], dy[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int i = base + tid + LT * u;
+        dx[u] = i < n ? rx[i] : 0.0;
+        dy[u] = i < n ? ry[i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int i = base + tid + LT * u;
+        if (i < n && i != y && live(mask, i)) {
+          const double nd = lw_update(method, dx[u], dy[u], nx, ny);
+          ry[i] = nd;
+          D[i * nn + y] = nd;
+        }
+      }
     }
     __syncthreads();
   }
 }
+
+// sklearn mst_linkage_core (Prim) over the rows of the symmetric D: out [n-1][3] = (current
+// node, new node, distance) per step; cur: the running minimum distance of every node ([n]
+// float64 workspace).
+__global__ __launch_bounds__(LT) void mst_kernel(const double* __restrict__ D, int n, double* __restrict__ out,
+                                                 double* __restrict__ cur) {
+  extern __shared__ unsigned tree[];  // in_tree, one bit per node
+  __shared__ double rv[LT / 64];
+  __shared__ int ri[LT / 64];
+  const int tid = threadIdx.x;
+  const int nw = (n + 31) >> 5;
+  constexpr double INF = __builtin_huge_val();
+  for (int i = tid; i < n; i += LT) cur[i] = INF;
+  for (int w = tid; w < nw; w += LT) tree[w] = 0u;
+  __syncthreads();
+  int node = 0;
+  for (int k = 0; k < n - 1; ++k) {
+    if (tid == 0) tree[node >> 5] |= 1u << (node & 31);
+    __syncthreads();
+    const double* row = D + static_cast<size_t>(node) * n;
+    double v = INF;
+    int bi = 0x7fffffff;
+    for (int base = 0; base < n; base += LT * NB) {
+      double l[NB], r[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int j = base + tid + LT * u;
+        l[u] = j < n ? row[j] : INF;
+        r[u] = j < n ? cur[j] : INF;
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int j = base + tid + LT * u;
+        if (j < n && !((tree[j >> 5] >> (j & 31)) & 1u)) {
+          double c = r[u];
+          if (l[u] < c) {  // left_value < right_value
+            c = l[u];
+            cur[j] = c;
+          }
+          if (c < v) {  // current_distances[j] < new_distance: the first minimum
+            v = c;
+            bi = j;
+          }
+        }
+      }
+    }
+    block_argmin(v, bi, rv, ri);
+    const int nxt = (v < INF) ? bi : 0;  // sklearn's new_node starts at 0
+    if (tid == 0) {
+      out[3 * static_cast<size_t>(k) + 0] = node;
+      out[3 * static_cast<size_t>(k) + 1] = nxt;
+      out[3 * static_cast<size_t>(k) + 2] = v;
+    }
+    node = nxt;
+    __syncthreads();  // cur[] of this step is written before the next step reads it
+  }
+}
+
+size_t mask_bytes(int n) { return static_cast<size_t>((n + 31) >> 5) * sizeof(unsigned); }
+
+// the dynamic LDS of the bitmask (up to the 160 KiB of a CU, less the static part)
+constexpr size_t MASK_LDS_MAX = 160 * 1024 - 1024;
 
 }  // namespace
 
@@ -246,16 +357,35 @@ extern "C" size_t cc_linkage_workspace_bytes(int n) {
 extern "C" int cc_linkage_nnchain(double* D, int n, int method, double* Z, void* workspace, size_t ws_bytes,
                                   void* stream) {
   if (!D || !Z || n < 2 || !workspace || ws_bytes < cc_linkage_workspace_bytes(n) ||
-      (method != CC_LINK_AVERAGE && method != CC_LINK_COMPLETE && method != CC_LINK_WEIGHTED)) {
+      (method != CC_LINK_AVERAGE && method != CC_LINK_COMPLETE && method != CC_LINK_WEIGHTED) ||
+      mask_bytes(n) > MASK_LDS_MAX) {
     cc::set_error("cc_linkage_nnchain: bad arguments");
     return CC_ERR_ARG;
   }
   int* size = static_cast<int*>(workspace);
-  hipLaunchKernelGGL(nnchain_kernel, dim3(1), dim3(LT), 0, static_cast<hipStream_t>(stream), D, n, method, Z, size,
-                     size + n);
+  hipLaunchKernelGGL(nnchain_kernel, dim3(1), dim3(LT), mask_bytes(n), static_cast<hipStream_t>(stream), D, n,
+                     method, Z, size, size + n);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     cc::set_error(std::string("cc_linkage_nnchain: ") + hipGetErrorString(e));
+    return CC_ERR_HIP;
+  }
+  return CC_OK;
+}
+
+extern "C" size_t cc_linkage_mst_workspace_bytes(int n) { return n > 0 ? static_cast<size_t>(n) * sizeof(double) : 0; }
+
+extern "C" int cc_linkage_mst(const double* D, int n, double* out, void* workspace, size_t ws_bytes, void* stream) {
+  if (!D || !out || n < 2 || !workspace || ws_bytes < cc_linkage_mst_workspace_bytes(n) ||
+      mask_bytes(n) > MASK_LDS_MAX) {
+    cc::set_error("cc_linkage_mst: bad arguments");
+    return CC_ERR_ARG;
+  }
+  hipLaunchKernelGGL(mst_kernel, dim3(1), dim3(LT), mask_bytes(n), static_cast<hipStream_t>(stream), D, n, out,
+                     static_cast<double*>(workspace));
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cc::set_error(std::string("cc_linkage_mst: ") + hipGetErrorString(e));
     return CC_ERR_HIP;
   }
   return CC_OK;

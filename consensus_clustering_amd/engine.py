@@ -257,6 +257,20 @@ def linkage(D: torch.Tensor, method: str) -> np.ndarray:
     return linkage_finish(Z.cpu().numpy(), n)
 
 
+def linkage_single(D: torch.Tensor) -> np.ndarray:
+    """sklearn's single-linkage tree of the rows behind the symmetric float64 [n, n] distances D
+    (device, read only): mst_linkage_core's Prim edges on the device (cc_linkage_mst), then the
+    stable sort and _single_linkage_label on the host (post.single_linkage_finish).  Z [n-1, 4]."""
+    assert D.dtype == torch.float64 and D.dim() == 2 and D.shape[0] == D.shape[1] and D.is_contiguous()
+    n = D.shape[0]
+    out = torch.empty((n - 1, 3), dtype=torch.float64, device=D.device)
+    ws = torch.empty(int(_lib.load().cc_linkage_mst_workspace_bytes(n)), dtype=torch.uint8, device=D.device)
+    _lib.call("cc_linkage_mst", D.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws.numel(), stream_ptr())
+    from .post import single_linkage_finish
+
+    return single_linkage_finish(out.cpu().numpy(), n)
+
+
 def manhattan(C: torch.Tensor) -> torch.Tensor:
     """float64 [n, n] manhattan distances between the rows of the float32 [n, n] C."""
     assert C.dtype == torch.float32 and C.dim() == 2 and C.is_contiguous()

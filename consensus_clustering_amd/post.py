@@ -130,3 +130,34 @@ def hc_cut(n_clusters, children, n_leaves):
                 stack.extend(children[v - n_leaves])
         label[leaves] = i
     return label
+
+
+def single_linkage_finish(mst, n):
+    """sklearn's single-linkage tree from mst_linkage_core's edges [n-1, 3] (current node, new
+    node, distance, in Prim order; sklearn/cluster/_agglomerative.py linkage_tree): the edges
+    sorted by distance (stable mergesort), then _hierarchical_fast._single_linkage_label: with
+    sklearn's UnionFind, each edge's two end points are renamed to their current clusters (left,
+    right, in that order: no min/max) and the merge creates cluster n + i.  Returns Z [n-1, 4]."""
+    L = np.asarray(mst, dtype=np.float64)
+    L = L[np.argsort(L[:, 2], kind="mergesort")]
+    parent = np.full(2 * n - 1, -1, dtype=np.int64)
+    size = np.zeros(2 * n - 1, dtype=np.int64)
+    size[:n] = 1
+    out = np.zeros((n - 1, 4), dtype=np.float64)
+
+    par = parent.tolist()
+
+    def find(x):  # UnionFind.fast_find: the root, with path compression
+        r = x
+        while par[r] != -1:
+            r = par[r]
+        while x != r and par[x] != r:
+            par[x], x = r, par[x]
+        return r
+
+    for i in range(n - 1):
+        lc, rc = find(int(L[i, 0])), find(int(L[i, 1]))
+        out[i] = (lc, rc, L[i, 2], size[lc] + size[rc])
+        par[lc] = par[rc] = n + i
+        size[n + i] = size[lc] + size[rc]
+    return out

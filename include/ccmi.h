@@ -173,6 +173,16 @@ size_t cc_linkage_workspace_bytes(int n);
 int cc_linkage_nnchain(double* D, int n, int method, double* Z, void* workspace, size_t ws_bytes,
                        void* stream);
 
+/* Single linkage of the consensus labels: sklearn's path for linkage='single' with the
+ * reference's 'manhattan' affinity (CC.py:306-312 -> linkage_tree ->
+ * _hierarchical_fast.mst_linkage_core, Prim's MST-LINKAGE-CORE) on the device, over the rows of
+ * D [n][n] float64 (read only; cc_manhattan's values are DistanceMetric64 cityblock's).
+ * out [n-1][3] float64 = (current node, new node, distance) per Prim step; the caller sorts the
+ * edges by distance (stable) and labels them (_single_linkage_label).  One workgroup; workspace
+ * of cc_linkage_mst_workspace_bytes(n) bytes. */
+size_t cc_linkage_mst_workspace_bytes(int n);
+int cc_linkage_mst(const double* D, int n, double* out, void* workspace, size_t ws_bytes, void* stream);
+
 /* Batched k-means for every (resample h, K, init) problem, replacing the per-(K, h)
  * clusterer.fit_predict(X[indices]) of CC.py:282 for the default clusterer
  * (sklearn KMeans: k-means++ init with 2+floor(ln K) local trials, Lloyd with strict

@@ -75,3 +75,59 @@ def test_predict_headline_n():
     # the cut's clusters are the planted blocks (a bijection)
     pairs = set(zip(lab.tolist(), gh.tolist()))
     assert len(pairs) == k and len({a for a, _ in pairs}) == k and len({b for _, b in pairs}) == k
+
+
+@pytest.mark.parametrize("n,seed,ties", [(2, 0, False), (3, 0, True), (257, 1, True), (1500, 2, False)])
+def test_device_mst_equals_oracle(n, seed, ties):
+    """cc_linkage_mst (sklearn's mst_linkage_core, the single-linkage path) equals the oracle's
+    restatement bit for bit, ties included."""
+    D = _distances(n, seed, ties)
+    Dd = torch.from_numpy(D).cuda()
+    out = torch.empty((n - 1, 3), dtype=torch.float64, device="cuda")
+    from consensus_clustering_amd import _lib
+
+    ws = torch.empty(int(_lib.load().cc_linkage_mst_workspace_bytes(n)), dtype=torch.uint8, device="cuda")
+    _lib.call("cc_linkage_mst", Dd.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws.numel(), engine.stream_ptr())
+    np.testing.assert_array_equal(out.cpu().numpy(), O.mst_prim(D))
+
+
+def test_predict_single_linkage_equals_sklearn():
+    """predict() with agg_clustering_linkage='single' (CC.py:306-312: AgglomerativeClustering(
+    linkage='single', affinity='manhattan') on the rows of C) on the device: identical labels to
+    sklearn's own fit on the same C."""
+    from sklearn.cluster import AgglomerativeClustering
+
+    from consensus_clustering_amd import ConsensusClustering
+    from tests.conftest import load_fixture
+
+    f = load_fixture("blobs_n400_d8_k4")
+    meta = f["meta"]
+    cc = ConsensusClustering(K_range=[int(k) for k in f["K_range"]], n_iterations=meta["H"],
+                             subsampling=meta["subsampling"], random_state=meta["random_state"],
+                             plot_cdf=False, agg_clustering_linkage="single").fit(f["X"])
+    for K in (2, 4, 6):
+        C = cc.cdf_at_K_data[K]["cij"]
+        want = AgglomerativeClustering(n_clusters=K, linkage="single", metric="manhattan").fit_predict(C)
+        np.testing.assert_array_equal(cc.predict(K), want, err_msg=f"K={K}")
+
+
+def test_single_linkage_headline_n():
+    """'single' linkage at n = 50 000 on the device (no host cap): the planted blocks of
+    test_predict_headline_n are recovered; prints the MST time."""
+    n, k = 50_000, 6
+    dev = torch.device("cuda")
+    g = torch.randint(0, k, (n,), generator=torch.Generator().manual_seed(0)).to(dev)
+    C = torch.where(g[:, None] == g[None, :], 0.9, 0.1).float()
+    C += torch.rand((n, n), generator=torch.Generator(device=dev).manual_seed(1), device=dev) * 0.05
+    C = torch.minimum(C, C.T).contiguous()
+    C.fill_diagonal_(1.0)
+    D = engine.manhattan(C)
+    del C
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    Z = engine.linkage_single(D)
+    t1 = time.perf_counter()
+    lab = post.hc_cut(k, Z[:, :2].astype(np.int64), n)
+    print(f"single linkage n={n}: mst + finish {t1 - t0:.2f} s")
+    pairs = set(zip(lab.tolist(), g.cpu().numpy().tolist()))
+    assert len(pairs) == k and len({a for a, _ in pairs}) == k and len({b for _, b in pairs}) == k

@@ -88,3 +88,17 @@ def test_native_kpp_first_centre_matches_numpy_choice(m, dtype):
         for i in range(3):
             assert pos[k, i] == rs.choice(m, p=sw / sw.sum())
             np.testing.assert_array_equal(u[k, i, 1:1 + (K - 1) * t], rs.random_sample((K - 1) * t))
+
+
+def test_numpy_argpartition_takes_distinct_farthest_first():
+    """sklearn's relocation (_k_means_common.pyx:187) takes np.argpartition(d, -k)[:-k-1:-1]; on
+    DISTINCT values this image's numpy returns the k largest in descending order for k <= 8, which
+    is the order cc_kmeans_f64 relocates in (farthest first).  Ties are pinned separately
+    (tests/test_gpu_kmeans.py::test_f64_relocation_with_ties_is_pinned)."""
+    rng = np.random.default_rng(1)
+    for _ in range(2000):
+        n = int(rng.integers(2, 3000))
+        k = int(rng.integers(1, min(n, 8) + 1))
+        a = rng.random(n)
+        got = np.argpartition(a, -k)[:-k - 1:-1]
+        np.testing.assert_array_equal(got, np.argsort(-a, kind="stable")[:k])
