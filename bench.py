@@ -88,17 +88,15 @@ def _timed_fit(X, idx_row, K):
 
     with threadpool_limits(1):
         t = time.perf_counter()
-        O.kmeans_labels(X[idx_row], K, SEED, n_init=3)
-        return time.perf_counter() - t
+        lab = O.kmeans_labels(X[idx_row], K, SEED, n_init=3)
+        return time.perf_counter() - t, lab
 
 
-def _timed_coassoc(n, idx_row, lab_seed, K, block):
-    """CC.py:284-290 for one (h, K) on a `block`-row slice of the n x n uint16 M: one-hot L,
-    the integer L^T L and the in-place add (one thread)."""
+def _timed_coassoc(n, idx_row, lab, K, block):
+    """CC.py:284-290 for one (h, K) on a `block`-row slice of the n x n uint16 M: one-hot L of
+    that fit's own labels, the integer L^T L and the in-place add (one thread)."""
     from threadpoolctl import threadpool_limits
 
-    rs = np.random.RandomState(lab_seed)
-    lab = rs.randint(0, K, size=len(idx_row))
     with threadpool_limits(1):
         L = np.zeros((K, n), dtype=np.uint16)
         L[lab, idx_row] = 1
@@ -136,12 +134,13 @@ def cpu_baseline(cfg, X, H_sample=8):
     print(f"[bench] cpu baseline: {cores} joblib processes", file=sys.stderr, flush=True)
     with Parallel(n_jobs=cores, prefer="processes") as par:
         a = time.perf_counter()
-        par(delayed(_timed_fit)(X, idx[h], K) for K in Ks for h in range(Hs))
+        fits = par(delayed(_timed_fit)(X, idx[h], K) for K in Ks for h in range(Hs))
         T_fits = (time.perf_counter() - a) * (H / Hs)
         print("[bench] cpu baseline: fits sampled", file=sys.stderr, flush=True)
         block = min(n, 1000)
         sampleK = sorted({Ks[0], Ks[len(Ks) // 2], Ks[-1]})
-        tco = par(delayed(_timed_coassoc)(n, idx[0], K, K, block) for K in sampleK)
+        lab0 = {K: fits[k * Hs][1] for k, K in enumerate(Ks)}  # resample 0's labels of each K
+        tco = par(delayed(_timed_coassoc)(n, idx[0], lab0[K], K, block) for K in sampleK)
     t_co = {K: t * (n / block) for K, t in zip(sampleK, tco)}
     T_co = sum(H * np.interp(K, sampleK, [t_co[k] for k in sampleK]) for K in Ks) / cores
     # I = S^T S (serial numpy integer matmul) and the per-K analysis, on row blocks
@@ -169,8 +168,8 @@ def cpu_baseline(cfg, X, H_sample=8):
                    f"{__import__('sklearn').__version__} KMeans n_init=3), joblib processes "
                    f"n_jobs={cores} x 1 BLAS thread (CC.py:185-195): all {len(Ks)} K x H'={Hs} "
                    f"resample fits timed ({T_fits * Hs / H:.1f} s wall), extrapolated x{H / Hs:.0f} "
-                   f"in H; co-association L^T L + add timed on a {block}-row block for K in "
-                   f"{sampleK} and scaled to n rows / n_jobs; S^T S ({bI}-row block) and "
+                   f"in H; co-association L^T L + add (the sampled fits' own labels) timed on a "
+                   f"{block}-row block for K in {sampleK} and scaled to n rows / n_jobs; S^T S ({bI}-row block) and "
                    f"C/histogram ({bA}-row block) serial, scaled to n rows. Extrapolated fit "
                    f"{total / 3600:.2f} h = I {T_I:.0f} s + fits {T_fits:.0f} s + co-association "
                    f"{T_co:.0f} s + analysis {T_an:.0f} s; sampled {time.perf_counter() - t0:.1f} s"),

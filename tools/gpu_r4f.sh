@@ -12,3 +12,7 @@ for c in "c2 16" "c3 8"; do
   CCMI_LIB=consensus_clustering_amd/libccmi_f64_base.so timeout -k 10 300 python -u tools/f64_ab.py $1 $2 $O/base_$1.npz 2>&1 | grep -v amdgpu || exit 1
   python tools/f64_ab.py --compare $O/new_$1.npz $O/base_$1.npz || exit 1
 done
+timeout -k 10 600 python -u tools/gmm_time.py 10000 16 32 > $O/gmm_time.txt 2>&1; grep -v amdgpu $O/gmm_time.txt
+# k-means compiler-scheduling variants (tools/build_variant.sh flags), C3 launch alone
+LIBS="libccmi_kv_base.so libccmi_kv_ptr.so libccmi_kv_trk.so libccmi_kv_nohrp.so libccmi_kv_bias0.so libccmi_kv_bias100.so libccmi_kv_noclo.so libccmi_kv_noDE.so libccmi_kv_base.so" KM_H=1000 KM_CFG=c3 bash tools/gpu_ab.sh 2>&1 | grep -v amdgpu | tee $O/kv_ab.txt
+for c in c3 c2; do timeout -k 10 120 python -u tools/rs_time.py $c 3 2>&1 | grep -v amdgpu | tee -a $O/rs_time.txt; done

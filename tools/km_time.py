@@ -2,6 +2,7 @@
 
     python tools/km_time.py [H] [config] [reps]
 """
+import hashlib
 import os
 import sys
 
@@ -36,7 +37,8 @@ for r in range(reps + 1):
     if r:
         ts.append(a.elapsed_time(b))
 print(os.path.basename(os.environ.get("CCMI_LIB", "libccmi.so")), "kmeans ms", [round(t, 1) for t in ts],
-      "sweeps", int(bk.stats[4]), "sparse item-sweeps", int(bk.stats[6]), "changes", int(bk.stats[7]), flush=True)
+      "sweeps", int(bk.stats[4]), "sparse item-sweeps", int(bk.stats[6]), "changes", int(bk.stats[7]),
+      "labels sha", hashlib.sha256(L.cpu().numpy().tobytes()).hexdigest()[:16], flush=True)
 st = bk.stats.cpu().numpy()
 cyc, cnt = st[80:89].astype(float), st[96:105].astype(float)
 tot = max(cyc.sum(), 1)
