@@ -36,6 +36,7 @@ import numpy as np
 import torch
 
 from . import dist, engine, post
+from ._hostfit import fit_predict_chunk, fit_predict_one
 from .kmeans import BatchedKMeans
 
 KMAX = 127  # largest K: uint8 labels (0xFF = not sampled) and int8 one-hot channels
@@ -485,7 +486,7 @@ def _clone(clusterer):
 
 
 def _fit_predict_one(clusterer, Xs):
-    return np.asarray(clusterer.fit_predict(Xs))
+    return fit_predict_one(clusterer, Xs)
 
 
 def host_fit_predict(clusterer, X, idx, n_jobs=1, parallelization_method='multithreading'):
@@ -498,24 +499,28 @@ def host_fit_predict(clusterer, X, idx, n_jobs=1, parallelization_method='multit
     RETURNED, not accumulated into a shared matrix, so the workers cannot race (the reference adds
     into one shared Mij from every worker); under threads each task fits its own copy of the
     clusterer (the reference shares one, whose fit_predict can return another thread's labels).
-    The labels do not depend on n_jobs."""
+    A process task carries a contiguous chunk of resamples (about four chunks per worker), and
+    its function lives in a module that does not import torch (_hostfit), so a worker starts
+    with sklearn alone.  The labels do not depend on n_jobs."""
     H = len(idx)
     if H == 0:
         return np.empty((0, 0), dtype=np.int32)
     if n_jobs == 1:
         return np.stack([_fit_predict_one(clusterer, X[i]) for i in idx]).astype(np.int32)
+    from joblib import Parallel, delayed, effective_n_jobs
+
     if parallelization_method == 'multithreading':
-        prefer = 'threads'
-        make = _clone
+        out = Parallel(n_jobs=n_jobs, prefer='threads')(
+            delayed(fit_predict_one)(_clone(clusterer), X[i]) for i in idx)
     elif parallelization_method == 'multiprocessing':
-        prefer = 'processes'
-        make = lambda c: c  # noqa: E731  (pickled per task by joblib)
+        chunks = max(1, min(H, 4 * effective_n_jobs(n_jobs)))
+        bounds = np.linspace(0, H, chunks + 1).astype(int)
+        parts = Parallel(n_jobs=n_jobs, prefer='processes')(
+            delayed(fit_predict_chunk)(clusterer, [X[i] for i in idx[a:b]])
+            for a, b in zip(bounds[:-1], bounds[1:]) if b > a)
+        out = [lab for part in parts for lab in part]
     else:
         raise RuntimeError(f'unknown parallelization method: {parallelization_method}')
-    from joblib import Parallel, delayed
-
-    out = Parallel(n_jobs=n_jobs, prefer=prefer)(
-        delayed(_fit_predict_one)(make(clusterer), X[i]) for i in idx)
     return np.stack(out).astype(np.int32)
 
 

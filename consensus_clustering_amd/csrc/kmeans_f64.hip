@@ -24,8 +24,15 @@
 //
 // Mapping: a persistent grid; one 256-thread workgroup runs one (resample, K) unit at a time
 // (all its inits, sequentially), with per-workgroup float64 scratch in the caller's workspace.
-// It is the precision path for float64 input, not the throughput path.
+// Round 4: the unit's centred rows are materialised once ([m][d] float64, the same subtraction),
+// every dot product runs as one of G (or ntr) independent sequential FMA chains per thread (a
+// thread's row against G centres at once: the same chain per value, G times the ILP), and the
+// centre sums walk per-cluster row lists built in row order (a ballot compaction), one thread
+// per (cluster, feature) with coalesced row reads instead of one thread per feature
+// read-modify-writing global sums row after row.  Every value keeps its sequential order, so
+// the results are bit-identical to the previous kernel (and to sklearn where it was).
 #include <hip/hip_runtime.h>
+#include <cstring>
 
 #include <algorithm>
 #include <cmath>
@@ -62,7 +69,7 @@ struct F64Args {
   unsigned* counter;
   char* ws;
   size_t per_wg;
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_ord;
 };
 
 // numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) of a contiguous double array:
@@ -196,29 +203,55 @@ __device__ double blas_gemv_t_ones(const double* x, int m, int col, int ncol) {
 }
 
 struct WG {
-  double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew;
-  int32_t *lab, *lold;
+  double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew, *xc;
+  int32_t *lab, *lold, *ord;
   uint8_t* lbest;
 };
+
+constexpr int G = 4;  // centres per E-step pass (independent FMA chains per thread)
+
+// The unit's centred row r (materialised: X[idx[r]][k] - mean[k], rounded once).
+__device__ __forceinline__ const double* xrow(const WG& w, int d, int r) { return w.xc + static_cast<size_t>(r) * d; }
+
+// The E-step argmin of row x over the K centres (|c|^2 in cn): G centres per pass, each
+// |c_j|^2 - 2 x.c_j with x.c_j the sequential FMA chain of dotc; strict < over increasing j.
+__device__ __forceinline__ int estep_row(const double* x, const double* cen, const double* cn, int K, int d) {
+  double best = 0.0;
+  int lab = 0;
+  for (int j0 = 0; j0 < K; j0 += G) {
+    double acc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc[g] = 0.0;
+    const int ng = K - j0 < G ? K - j0 : G;
+    for (int k = 0; k < d; ++k) {
+      const double xk = x[k];
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+        if (g < ng) acc[g] = __fma_rn(xk, cen[static_cast<size_t>(j0 + g) * d + k], acc[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (g >= ng) break;
+      const int j = j0 + g;
+      const double dj = __fma_rn(-2.0, acc[g], cn[j]);
+      if (j == 0 || dj < best) {
+        best = dj;
+        lab = j;
+      }
+    }
+  }
+  return lab;
+}
 
 // centred feature k of resample row r
 __device__ __forceinline__ double xc(const F64Args& a, const int32_t* idx, const double* mean, int r, int k) {
   return a.X[static_cast<size_t>(idx[r]) * a.d + k] - mean[k];
 }
 
-__device__ double dotc(const F64Args& a, const int32_t* idx, const double* mean, int r, const double* c) {
-  double s = 0.0;
-  for (int k = 0; k < a.d; ++k) s = __fma_rn(xc(a, idx, mean, r, k), c[k], s);
-  return s;
-}
-
-__device__ double dotrr(const F64Args& a, const int32_t* idx, const double* mean, int r, int q) {
-  double s = 0.0;
-  for (int k = 0; k < a.d; ++k) s = __fma_rn(xc(a, idx, mean, r, k), xc(a, idx, mean, q, k), s);
-  return s;
-}
-
-__global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
+__global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restrict__ pa) {
+  // arguments read from the workspace header (as in kmeans.hip): re-loaded where used rather
+  // than pinned in SGPRs for the whole kernel
+  const F64Args& a = *pa;
   __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[TMAX], s_map[KMAX + 1];
   __shared__ double s_pot[TMAX], s_tol, s_red[NT];
   __shared__ int s_ired[NT];
@@ -235,6 +268,9 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
   w.lab = reinterpret_cast<int32_t*>(base + a.o_lab);
   w.lold = reinterpret_cast<int32_t*>(base + a.o_lold);
   w.lbest = reinterpret_cast<uint8_t*>(base + a.o_lbest);
+  w.xc = reinterpret_cast<double*>(base + a.o_xc);
+  w.ord = reinterpret_cast<int32_t*>(base + a.o_ord);
+  __shared__ int s_off[KMAX + 2];
   const int m = a.m, d = a.d;
   for (;;) {
     __syncthreads();
@@ -263,9 +299,17 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
     }
     __syncthreads();
     if (tid == 0) s_tol = (np_pairwise(w.sq, d) / d) * a.tol_rel;
+    // the centred rows, once per unit (the values every later step reads)
+    for (size_t e = tid; e < static_cast<size_t>(m) * d; e += NT) {
+      const int r = static_cast<int>(e / d), k = static_cast<int>(e - static_cast<size_t>(r) * d);
+      w.xc[e] = xc(a, idx, w.mean, r, k);
+    }
+    __syncthreads();
     // squared row norms of the centred rows
-    for (int r = tid; r < m; r += NT)
-      w.xsq[r] = einsum_sq([&](int k) { return xc(a, idx, w.mean, r, k); }, d);
+    for (int r = tid; r < m; r += NT) {
+      const double* x = xrow(w, d, r);
+      w.xsq[r] = einsum_sq([&](int k) { return x[k]; }, d);
+    }
     __syncthreads();
     const double tol = s_tol;
 
@@ -275,9 +319,13 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
       const double* u = a.kpp_u + (static_cast<size_t>(kk) * a.n_init + init) * a.kpp_stride + 1;
       // ---- k-means++ -------------------------------------------------------------
       int cpos = a.kpp_pos[kk * a.n_init + init];
-      for (int k = tid; k < d; k += NT) w.cen[k] = xc(a, idx, w.mean, cpos, k);
+      for (int k = tid; k < d; k += NT) w.cen[k] = xrow(w, d, cpos)[k];
       for (int r = tid; r < m; r += NT) {
-        double dd = -2.0 * dotrr(a, idx, w.mean, cpos, r);
+        const double* xq = xrow(w, d, cpos);
+        const double* xr = xrow(w, d, r);
+        double s0 = 0.0;
+        for (int k = 0; k < d; ++k) s0 = __fma_rn(xq[k], xr[k], s0);
+        double dd = -2.0 * s0;
         dd += w.xsq[cpos];
         dd += w.xsq[r];
         w.cl[r] = dd > 0.0 ? dd : 0.0;
@@ -303,9 +351,26 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
         }
         __syncthreads();
         for (int r = tid; r < m; r += NT) {
-          for (int t = 0; t < ntr; ++t) {
+          // the ntr candidates' dot products as independent sequential FMA chains
+          const double* xr = xrow(w, d, r);
+          const double* xq[TMAX];
+          double acc[TMAX];
+#pragma unroll
+          for (int t = 0; t < TMAX; ++t) {
+            xq[t] = xrow(w, d, s_cand[t < ntr ? t : 0]);
+            acc[t] = 0.0;
+          }
+          for (int k = 0; k < d; ++k) {
+            const double xk = xr[k];
+#pragma unroll
+            for (int t = 0; t < TMAX; ++t)
+              if (t < ntr) acc[t] = __fma_rn(xq[t][k], xk, acc[t]);
+          }
+#pragma unroll
+          for (int t = 0; t < TMAX; ++t) {
+            if (t >= ntr) break;
             const int q = s_cand[t];
-            double dd = -2.0 * dotrr(a, idx, w.mean, q, r);
+            double dd = -2.0 * acc[t];
             dd += w.xsq[q];
             dd += w.xsq[r];
             dd = dd > 0.0 ? dd : 0.0;
@@ -321,7 +386,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
         pot = s_pot[bt];
         cpos = s_cand[bt];
         for (int r = tid; r < m; r += NT) w.cl[r] = w.dc[static_cast<size_t>(bt) * m + r];
-        for (int k = tid; k < d; k += NT) w.cen[static_cast<size_t>(c) * d + k] = xc(a, idx, w.mean, cpos, k);
+        for (int k = tid; k < d; k += NT) w.cen[static_cast<size_t>(c) * d + k] = xrow(w, d, cpos)[k];
         __syncthreads();
       }
       // ---- Lloyd -------------------------------------------------------------------
@@ -339,28 +404,59 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
         }
         __syncthreads();
         int chg = 0;
+        for (int j = tid; j < K; j += NT) s_ired[j] = 0;
+        __syncthreads();
         for (int r = tid; r < m; r += NT) {
-          double best = 0.0;
-          int lab = 0;
-          for (int j = 0; j < K; ++j) {
-            const double dj = __fma_rn(-2.0, dotc(a, idx, w.mean, r, cen + static_cast<size_t>(j) * d), s_red[j]);
-            if (j == 0 || dj < best) {
-              best = dj;
-              lab = j;
-            }
-          }
+          const int lab = estep_row(xrow(w, d, r), cen, s_red, K, d);
           w.lab[r] = lab;
           chg |= (lab != w.lold[r]);
+          atomicAdd(&s_ired[lab], 1);  // counts (integers: order-free)
         }
         const int changed = __syncthreads_or(chg);
-        // centre sums in row order: thread per feature
-        for (int k = tid; k < d; k += NT) {
-          for (int j = 0; j < K; ++j) cnew[static_cast<size_t>(j) * d + k] = 0.0;
-          for (int r = 0; r < m; ++r) cnew[static_cast<size_t>(w.lab[r]) * d + k] += xc(a, idx, w.mean, r, k);
-        }
+        // centre sums in row order: the rows of each cluster listed in row order (offsets by
+        // cluster, then one wave per cluster compacting 64 rows per ballot), then one thread per
+        // (cluster, feature) summing its list sequentially: the same additions, in the same order,
+        // as sklearn's row loop
         if (tid == 0) {
-          for (int j = 0; j < K; ++j) s_ired[j] = 0;
-          for (int r = 0; r < m; ++r) s_ired[w.lab[r]] += 1;
+          int o = 0;
+          for (int j = 0; j < K; ++j) {
+            s_off[j] = o;
+            o += s_ired[j];
+          }
+          s_off[K] = o;
+        }
+        __syncthreads();
+        {
+          const int wv = tid >> 6, ln = tid & 63;
+          for (int j = wv; j < K; j += NT / 64) {
+            int pos = s_off[j];
+            for (int b = 0; b < m; b += 64) {
+              const int r = b + ln;
+              const bool hit = r < m && w.lab[r] == j;
+              const unsigned long long msk = __ballot(hit);
+              if (hit) w.ord[pos + __popcll(msk & ((1ull << ln) - 1ull))] = r;
+              pos += __popcll(msk);
+            }
+          }
+        }
+        __syncthreads();
+        for (int p = tid; p < K * d; p += NT) {
+          const int j = p / d, k = p - (p / d) * d;
+          const int i0 = s_off[j], i1 = s_off[j + 1];
+          double sum = 0.0;
+          int i = i0;
+          for (; i + 8 <= i1; i += 8) {  // the loads of 8 rows in flight, added in order
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = xrow(w, d, w.ord[i + u])[k];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) sum += v[u];
+          }
+          for (; i < i1; ++i) sum += xrow(w, d, w.ord[i])[k];
+          cnew[static_cast<size_t>(j) * d + k] = sum;
+        }
+        __syncthreads();
+        if (tid == 0) {
           int ne = 0;
           for (int j = 0; j < K; ++j) ne += (s_ired[j] == 0);
           s_flag = ne;
@@ -376,24 +472,24 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
             double s = 0.0;
             if (d < 8) {
               for (int k = 0; k < d; ++k) {
-                const double e = xc(a, idx, w.mean, r, k) - c[k];
+                const double e = xrow(w, d, r)[k] - c[k];
                 s += e * e;
               }
             } else {
               double v[8];
               for (int q = 0; q < 8; ++q) {
-                const double e = xc(a, idx, w.mean, r, q) - c[q];
+                const double e = xrow(w, d, r)[q] - c[q];
                 v[q] = e * e;
               }
               int k = 8;
               for (; k < d - (d % 8); k += 8)
                 for (int q = 0; q < 8; ++q) {
-                  const double e = xc(a, idx, w.mean, r, k + q) - c[k + q];
+                  const double e = xrow(w, d, r)[k + q] - c[k + q];
                   v[q] += e * e;
                 }
               s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
               for (; k < d; ++k) {
-                const double e = xc(a, idx, w.mean, r, k) - c[k];
+                const double e = xrow(w, d, r)[k] - c[k];
                 s += e * e;
               }
             }
@@ -425,7 +521,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
             __syncthreads();
             const int far = s_best[0], j = s_map[e], old = w.lab[far];
             for (int k = tid; k < d; k += NT) {
-              const double x = xc(a, idx, w.mean, far, k);
+              const double x = xrow(w, d, far)[k];
               cnew[static_cast<size_t>(old) * d + k] -= x;
               cnew[static_cast<size_t>(j) * d + k] = x;
             }
@@ -458,7 +554,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
         // shifts and convergence
         if (tid < K) {
           const double sh = sqrt(euclid4(cnew + static_cast<size_t>(tid) * d, cen + static_cast<size_t>(tid) * d, d));
-          s_red[NT - 1 - tid] = sh * sh;
+          s_red[tid] = sh * sh;  // (the |c|^2 of this iteration are no longer read)
         }
         __syncthreads();
         double* tmp = cen;
@@ -468,9 +564,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
           strict = true;
           break;
         }
-        double shifts[KMAX];
-        for (int j = 0; j < K; ++j) shifts[j] = s_red[NT - 1 - j];
-        const double tot = np_pairwise(shifts, K);
+        const double tot = np_pairwise(s_red, K);
         for (int r = tid; r < m; r += NT) w.lold[r] = w.lab[r];
         if (tot <= tol) break;
       }
@@ -482,34 +576,24 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
           s_red[j] = einsum_sq([&](int k) { return cj[k]; }, d);
         }
         __syncthreads();
-        for (int r = tid; r < m; r += NT) {
-          double best = 0.0;
-          int lab = 0;
-          for (int j = 0; j < K; ++j) {
-            const double dj = __fma_rn(-2.0, dotc(a, idx, w.mean, r, cen + static_cast<size_t>(j) * d), s_red[j]);
-            if (j == 0 || dj < best) {
-              best = dj;
-              lab = j;
-            }
-          }
-          w.lab[r] = lab;
-        }
+        for (int r = tid; r < m; r += NT) w.lab[r] = estep_row(xrow(w, d, r), cen, s_red, K, d);
         __syncthreads();
       }
       // inertia: per-row squared distance to its centre, summed in row order
       for (int r = tid; r < m; r += NT) {
         const double* c = cen + static_cast<size_t>(w.lab[r]) * d;
+        const double* x = xrow(w, d, r);
         double res = 0.0;
         const int n4 = d / 4, rem = d % 4;
         for (int i = 0; i < n4; ++i) {
-          const double d0 = xc(a, idx, w.mean, r, 4 * i) - c[4 * i];
-          const double d1 = xc(a, idx, w.mean, r, 4 * i + 1) - c[4 * i + 1];
-          const double d2 = xc(a, idx, w.mean, r, 4 * i + 2) - c[4 * i + 2];
-          const double d3 = xc(a, idx, w.mean, r, 4 * i + 3) - c[4 * i + 3];
+          const double d0 = x[4 * i] - c[4 * i];
+          const double d1 = x[4 * i + 1] - c[4 * i + 1];
+          const double d2 = x[4 * i + 2] - c[4 * i + 2];
+          const double d3 = x[4 * i + 3] - c[4 * i + 3];
           res += ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;
         }
         for (int i = 0; i < rem; ++i) {
-          const double t = xc(a, idx, w.mean, r, 4 * n4 + i) - c[4 * n4 + i];
+          const double t = x[4 * n4 + i] - c[4 * n4 + i];
           res += t * t;
         }
         w.sq[r] = res;
@@ -556,7 +640,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(F64Args a) {
 }
 
 struct F64Layout {
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, per_wg;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_ord, per_wg;
 };
 
 F64Layout f64_layout(int m, int d, int kmax) {
@@ -573,11 +657,14 @@ F64Layout f64_layout(int m, int d, int kmax) {
   L.o_lab = o;   o += al(sizeof(int32_t) * m);
   L.o_lold = o;  o += al(sizeof(int32_t) * m);
   L.o_lbest = o; o += al(m);
+  L.o_xc = o;    o += al(sizeof(double) * static_cast<size_t>(m) * d);
+  L.o_ord = o;   o += al(sizeof(int32_t) * m);
   L.per_wg = o;
   return L;
 }
 
-constexpr size_t WS_HEADER = 256;
+constexpr size_t WS_ARGS = 64;  // the work counter at 0, the kernel's F64Args at WS_ARGS
+constexpr size_t WS_HEADER = (WS_ARGS + sizeof(F64Args) + 255) / 256 * 256;
 
 }  // namespace
 
@@ -621,11 +708,6 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
     return CC_ERR_ARG;
   }
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  hipError_t e = hipMemsetAsync(workspace, 0, sizeof(unsigned), st);
-  if (e != hipSuccess) {
-    cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));
-    return CC_ERR_HIP;
-  }
   F64Args a{};
   a.X = X;
   a.n = n;
@@ -660,8 +742,20 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.o_lab = L.o_lab;
   a.o_lold = L.o_lold;
   a.o_lbest = L.o_lbest;
+  a.o_xc = L.o_xc;
+  a.o_ord = L.o_ord;
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nK));
-  hipLaunchKernelGGL(kmeans_f64_kernel, dim3(blocks), dim3(NT), 0, st, a);
+  // one upload: the zeroed counter and the arguments (a pageable source is consumed before
+  // hipMemcpyAsync returns)
+  alignas(16) unsigned char header[WS_ARGS + sizeof(F64Args)] = {};
+  std::memcpy(header + WS_ARGS, &a, sizeof(F64Args));
+  hipError_t e = hipMemcpyAsync(workspace, header, sizeof(header), hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) {
+    cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));
+    return CC_ERR_HIP;
+  }
+  hipLaunchKernelGGL(kmeans_f64_kernel, dim3(blocks), dim3(NT), 0, st,
+                     reinterpret_cast<const F64Args*>(static_cast<char*>(workspace) + WS_ARGS));
   e = hipGetLastError();
   if (e != hipSuccess) {
     cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));

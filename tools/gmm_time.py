@@ -22,7 +22,7 @@ d = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 H = int(sys.argv[3]) if len(sys.argv) > 3 else 32
 X = make_blobs_f32(n, d, 5, seed=0).astype(np.float64)
 res = {}
-for n_jobs, method in ((1, "multithreading"), (16, "multithreading"), (16, "multiprocessing")):
+for n_jobs, method in ((1, "multithreading"), (16, "multithreading"), (16, "multiprocessing"), (16, "multiprocessing")):
     cc = ConsensusClustering(clusterer=GaussianMixture(n_init=2), K_range=range(2, 7), n_iterations=H,
                              random_state=0, plot_cdf=False, n_jobs=n_jobs, parallelization_method=method,
                              keep_matrices=False)
@@ -30,9 +30,9 @@ for n_jobs, method in ((1, "multithreading"), (16, "multithreading"), (16, "mult
         t0 = time.perf_counter()
         cc.fit(X)
         dt = time.perf_counter() - t0
-    res[(n_jobs, method)] = (dt, cc.labels_.cpu().numpy())
+    res[(n_jobs, method, len(res))] = (dt, cc.labels_.cpu().numpy())
     print(f"n={n} d={d} H={H} K=2..6 GaussianMixture(n_init=2): n_jobs={n_jobs} {method}: fit {dt:.2f} s "
           f"(host fits {cc.timings_['cluster']:.2f} s)", flush=True)
-base = res[(1, "multithreading")][1]
+base = res[(1, "multithreading", 0)][1]
 print("labels identical across n_jobs / methods:",
       all(np.array_equal(base, v[1]) for v in res.values()))

@@ -8,9 +8,9 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity_blobs.py::test_float
 rc=$?; grep -E "passed|failed|FAILED|float64 input|f64 relocation" $O/tests.log | tail -10; [ $rc -eq 0 ] || exit $rc
 for c in "c2 16" "c3 8"; do
   set -- $c
-  timeout -k 10 300 python -u tools/f64_ab.py $1 $2 $O/new_$1.npz 2>&1 | grep -v amdgpu || exit 1
-  CCMI_LIB=consensus_clustering_amd/libccmi_f64_base.so timeout -k 10 300 python -u tools/f64_ab.py $1 $2 $O/base_$1.npz 2>&1 | grep -v amdgpu || exit 1
-  python tools/f64_ab.py --compare $O/new_$1.npz $O/base_$1.npz || exit 1
+  timeout -k 10 300 python -u tools/f64_ab.py $1 $2 /tmp/new_$1.npz 2>&1 | grep -v amdgpu || exit 1
+  CCMI_LIB=consensus_clustering_amd/libccmi_f64_base.so timeout -k 10 300 python -u tools/f64_ab.py $1 $2 /tmp/base_$1.npz 2>&1 | grep -v amdgpu || exit 1
+  python tools/f64_ab.py --compare /tmp/new_$1.npz /tmp/base_$1.npz || exit 1
 done
 timeout -k 10 600 python -u tools/gmm_time.py 10000 16 32 > $O/gmm_time.txt 2>&1; grep -v amdgpu $O/gmm_time.txt
 # k-means compiler-scheduling variants (tools/build_variant.sh flags), C3 launch alone
