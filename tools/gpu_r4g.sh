@@ -21,3 +21,9 @@ for c in c5 c2 c4; do
   timeout -k 10 400 python -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_$c.json 2> $O/bench_$c.err || { echo "FAIL $c"; tail -3 $O/bench_$c.err; exit 1; }
   python -c "import json;d=json.loads(open('$O/bench_$c.json').read().strip().splitlines()[-1]);print('$c', round(d['ms_per_step'],1), d['value'], d['roofline']['frac'], d.get('roofline_coassoc',{}).get('frac'))"
 done
+# units per resample at one rank's load of 8 (default: choose_subsets)
+for ns in 1 3 4; do
+  CCMI_NSUB=$ns timeout -k 10 300 python -u bench.py --rehearse 0/8 --steps 2 --warmup 1 --no-cpu-baseline > $O/rehearse_0_8_nsub$ns.json 2> $O/rehearse_0_8_nsub$ns.err || { echo "FAIL nsub $ns"; exit 1; }
+  python -c "import json;d=json.loads(open('$O/rehearse_0_8_nsub$ns.json').read().strip().splitlines()[-1]);print('nsub $ns', round(d['ms_per_step'],1), {k: round(v,1) for k,v in d['kernels_ms_per_step'].items()})"
+done
+timeout -k 10 600 python -u tools/gmm_time.py 10000 16 32 > $O/gmm_time.txt 2>&1; grep -v amdgpu $O/gmm_time.txt
