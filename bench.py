@@ -54,6 +54,7 @@ CONFIGS = {
 F16_MFMA_PEAK_TF = 2516.6
 KMEANS_PEAK_TF = F16_MFMA_PEAK_TF / 3
 I8_MFMA_PEAK_TOPS = 2 * F16_MFMA_PEAK_TF  # v_mfma_i32_32x32x32_i8: 2x the f16 rate
+FP4_MFMA_PEAK_TOPS = 4 * F16_MFMA_PEAK_TF  # v_mfma_scale_f32_32x32x64_f8f6f4, e2m1: 4x the f16 rate
 SEED = 0
 
 
@@ -314,8 +315,11 @@ def main():
     st = stats.to(torch.float64)
     km_kernel = "cc_kmeans_batched" if cfg["d"] <= 128 else "cc_kmeans_wide"
     km_launch, km_ms = timers.get(km_kernel, (0, 0.0))
-    co_launch, co_ms = timers.get("cc_coassoc", (0, 0.0))
-    ktime = torch.tensor([km_ms, float(km_launch), co_ms], dtype=torch.float64, device=dev)
+    co_launch, co_ms_launches = timers.get("cc_coassoc", (0, 0.0))
+    # the per-K launches overlap on side streams (engine.coassoc_all): the band's span on the
+    # fit's stream is the co-association time; the sum of launch durations is reported beside it
+    co_ms = timers["coassoc_band"][1] if "coassoc_band" in timers else co_ms_launches
+    ktime = torch.tensor([km_ms, float(km_launch), co_ms, co_ms_launches], dtype=torch.float64, device=dev)
     if world > 1:
         tdist.all_reduce(vec, op=tdist.ReduceOp.MAX)
         tdist.all_reduce(st, op=tdist.ReduceOp.SUM)
@@ -343,13 +347,18 @@ def main():
         P = float(band_pairs(n_, tb_, te_))
     else:
         P = n_ * (n_ - 1) / 2
-    co_ops_t = torch.tensor([sum(2.0 * P * cfg["H"] * K for K in cfg["Ks"]) * args.steps],
+    # K = 2 runs the i8 MFMA, K >= 3 the FP4 form (4x the bf16 rate): the time the credited ops
+    # would take at the peak of the instruction each K actually issues
+    co_ops_t = torch.tensor([sum(2.0 * P * cfg["H"] * K for K in cfg["Ks"]) * args.steps,
+                             sum(2.0 * P * cfg["H"] * K / (I8_MFMA_PEAK_TOPS if K <= 2 else FP4_MFMA_PEAK_TOPS)
+                                 for K in cfg["Ks"]) * args.steps],
                             dtype=torch.float64, device=dev)
     if world > 1:
         tdist.all_reduce(co_ops_t, op=tdist.ReduceOp.SUM)
     co_ops = float(co_ops_t[0])
     co_ms_tot = float(ktime[2])
     co_achieved = co_ops / (co_ms_tot * 1e-3) / 1e12 if co_ms_tot > 0 else 0.0
+    co_frac_issued = float(co_ops_t[1]) / 1e12 / (co_ms_tot * 1e-3) if co_ms_tot > 0 else 0.0
     # per-config traffic files hold full single-GPU fits: not valid for a partial (rehearsal) run
     full_fit = not args.rehearse
 
@@ -399,6 +408,9 @@ def main():
                 "frac": checked_frac(co_achieved, I8_MFMA_PEAK_TOPS, "co-association"),
                 "ops_per_fit": co_ops / args.steps,
                 "ms_per_fit": co_ms_tot / args.steps,
+                "launch_ms_sum_per_fit": float(ktime[3]) / args.steps,
+                "frac_of_issued_instruction_peak": co_frac_issued,
+                "issued_peak_note": "K = 2: i8 MFMA 5033 TOP/s; K >= 3: FP4 v_mfma_scale_f32_32x32x64_f8f6f4 10066 TOP/s",
                 "traffic": (load_traffic(args.config, "cc_coassoc", key="bytes_per_fit")
                             if full_fit and world == 1 else None),
                 "note": "the 20-bin histogram (K5) is fused into this kernel's epilogue: no HBM pass",

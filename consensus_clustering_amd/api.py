@@ -29,6 +29,7 @@ Additions: ``cdf_area_``, ``delta_k_``, ``pac_area_``, ``best_k_`` and ``predict
 """
 from __future__ import annotations
 
+import os
 import time
 import warnings
 
@@ -267,13 +268,12 @@ class ConsensusClustering:
         nt = engine.num_tiles(n)
         t0, t1 = dist.shard(nt, rank, W)
         I_tiles, I_full = engine.cosample(labels[0], n, Hpad, t0, t1, want_full=keep)
-        edges = engine.edges_device(dev)
         counts = torch.zeros((len(Ks), post.N_BINS), dtype=torch.int64, device=dev)
         M_full = [None] * len(Ks)
-        for k, K in enumerate(Ks):
-            if keep:
-                M_full[k] = torch.zeros((n, n), dtype=torch.int32, device=dev)
-            engine.coassoc(labels[k], n, Hpad, K, t0, t1, I_tiles, edges, counts[k], M_full[k])
+        if keep:
+            M_full = [torch.zeros((n, n), dtype=torch.int32, device=dev) for _ in Ks]
+        engine.coassoc_all(labels, n, Hpad, Ks, t0, t1, I_tiles, counts, M_full if keep else None,
+                           streams=int(os.environ.get("CCMI_CO_STREAMS", 3)))
         dist.sum_counts(counts)
         if keep:
             dist.sum_counts(I_full)
@@ -507,7 +507,7 @@ def host_fit_predict(clusterer, X, idx, n_jobs=1, parallelization_method='multit
         return np.empty((0, 0), dtype=np.int32)
     if n_jobs == 1:
         return np.stack([_fit_predict_one(clusterer, X[i]) for i in idx]).astype(np.int32)
-    from joblib import Parallel, delayed, effective_n_jobs
+    from joblib import Parallel, delayed, effective_n_jobs, parallel_config
 
     if parallelization_method == 'multithreading':
         out = Parallel(n_jobs=n_jobs, prefer='threads')(
@@ -515,9 +515,13 @@ def host_fit_predict(clusterer, X, idx, n_jobs=1, parallelization_method='multit
     elif parallelization_method == 'multiprocessing':
         chunks = max(1, min(H, 4 * effective_n_jobs(n_jobs)))
         bounds = np.linspace(0, H, chunks + 1).astype(int)
-        parts = Parallel(n_jobs=n_jobs, prefer='processes')(
-            delayed(fit_predict_chunk)(clusterer, [X[i] for i in idx[a:b]])
-            for a, b in zip(bounds[:-1], bounds[1:]) if b > a)
+        # one BLAS thread per worker: loky would give each worker cpu_count // n_jobs threads,
+        # and cpu_count is the whole machine's on a shared node (16 workers x 16 threads on a
+        # 16-CPU share measured 7x slower than the serial loop)
+        with parallel_config(backend='loky', inner_max_num_threads=1):
+            parts = Parallel(n_jobs=n_jobs)(
+                delayed(fit_predict_chunk)(clusterer, [X[i] for i in idx[a:b]])
+                for a, b in zip(bounds[:-1], bounds[1:]) if b > a)
         out = [lab for part in parts for lab in part]
     else:
         raise RuntimeError(f'unknown parallelization method: {parallelization_method}')

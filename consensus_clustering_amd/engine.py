@@ -223,6 +223,46 @@ def coassoc(labels_nh: torch.Tensor, n: int, Hpad: int, K: int, tile_begin: int,
                   stream_ptr())
 
 
+_SIDE_STREAMS = {}
+
+
+def side_streams(device, count: int):
+    """`count` cached HIP streams of `device` for independent launches (the per-K co-association
+    launches of a fit): a launch covers only the tiles of one K, so at small n its last round of
+    tiles leaves CUs idle that the next K's launch can fill."""
+    key = str(device)
+    have = _SIDE_STREAMS.setdefault(key, [])
+    while len(have) < count:
+        have.append(torch.cuda.Stream(device=device))
+    return have[:count]
+
+
+def coassoc_all(labels: torch.Tensor, n: int, Hpad: int, Ks, tile_begin: int, tile_end: int,
+                I_tiles: torch.Tensor, counts: torch.Tensor, M_full=None, streams: int = 2):
+    """coassoc for every K (labels[k], counts[k], M_full[k]), the launches dealt round robin over
+    `streams` side streams forked from and joined back into the current stream.  The K are
+    independent (own label matrix, own counters), so the results do not depend on the overlap."""
+    dev = labels.device
+    edges = edges_device(dev)
+    bin_table(dev, Hpad + 1)  # staged once on the current stream, before any side stream reads it
+    main = torch.cuda.current_stream(dev)
+    if streams <= 1 or len(Ks) <= 1:
+        for k, K in enumerate(Ks):
+            coassoc(labels[k], n, Hpad, K, tile_begin, tile_end, I_tiles, edges, counts[k],
+                    None if M_full is None else M_full[k])
+        return
+    ss = side_streams(dev, min(int(streams), len(Ks)))
+    with timed("coassoc_band"):
+        for s in ss:
+            s.wait_stream(main)
+        for k, K in enumerate(Ks):
+            with torch.cuda.stream(ss[k % len(ss)]):
+                coassoc(labels[k], n, Hpad, K, tile_begin, tile_end, I_tiles, edges, counts[k],
+                        None if M_full is None else M_full[k])
+        for s in ss:
+            main.wait_stream(s)
+
+
 def consensus(M: torch.Tensor, I: torch.Tensor) -> torch.Tensor:
     n = M.shape[0]
     C = torch.empty((n, n), dtype=torch.float32, device=M.device)

@@ -241,3 +241,23 @@ def test_exact_k_packing_every_k(n, H, frac, pack, monkeypatch):
         C = O.consensus_matrix(M_ref.astype(np.uint16), I_ref.astype(np.uint16))
         pair, _ = np.histogram(C[iu], bins=20, range=(0, 1))
         np.testing.assert_array_equal(counts[j], pair, err_msg=f"K={K}")
+
+
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_coassoc_all_streams_is_exact(streams):
+    """The fit's per-K launches dealt over side streams (engine.coassoc_all) give the same
+    counts and M as one launch after the other, and as the oracle's histogram."""
+    dev = engine.require_gpu()
+    n, H, frac, Ks = 700, 90, 0.8, [2, 3, 5, 8, 13]
+    idx, labels = _random_case(n, H, frac, Ks, seed=11)
+    L, Hpad = _device_labels(idx, labels, n, H, dev)
+    I_ref, M_ref, counts_ref = _run(L, n, Hpad, Ks)
+    nt = engine.num_tiles(n)
+    I_tiles, _ = engine.cosample(L[0], n, Hpad, 0, nt)
+    counts = torch.zeros((len(Ks), 20), dtype=torch.int64, device=dev)
+    Ms = [torch.zeros((n, n), dtype=torch.int32, device=dev) for _ in Ks]
+    engine.coassoc_all(L, n, Hpad, Ks, 0, nt, I_tiles, counts, Ms, streams=streams)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(counts.cpu().numpy(), counts_ref)
+    for j in range(len(Ks)):
+        np.testing.assert_array_equal(Ms[j].cpu().numpy(), M_ref[j])
