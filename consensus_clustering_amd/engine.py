@@ -91,12 +91,15 @@ def resample_indices(seed: int, n: int, m: int, h_begin: int, h_end: int, n_thre
 RESAMPLE_WIDE_WS = 4 << 30
 
 
+RESAMPLE_SWAP_MAX_AUTO = 16384  # 'auto' uses the LDS swap chain up to this n, the wide form above
+
+
 def resample_indices_device(seed: int, n: int, m: int, h_begin: int, h_end: int, device,
                             out: torch.Tensor | None = None, method: str = "auto") -> torch.Tensor:
     """int32 [h_end-h_begin, m] on the device: the same draws as resample_indices.
     method 'swap': cc_resample_device (the shuffle simulated in LDS; n <= 65536); 'wide':
     cc_resample_device_wide (any n, resolved from the swap partners); 'auto': wide when
-    n > 65536 else swap.  `out`: a contiguous int32 device tensor of that shape to fill (e.g. a
+    n > 16384 (faster from there: C3 n = 50k 7.3 against 24.7 ms; equal at n = 10k) else swap.  `out`: a contiguous int32 device tensor of that shape to fill (e.g. a
     row slice of the full [H, m] matrix)."""
     if seed is None:
         raise TypeError("unsupported operand type(s) for +: 'NoneType' and 'int'")
@@ -109,7 +112,7 @@ def resample_indices_device(seed: int, n: int, m: int, h_begin: int, h_end: int,
           or not out.is_cuda):
         raise ValueError("out must be a contiguous int32 device tensor of shape [h_end - h_begin, m]")
     if method == "auto":
-        method = "wide" if n > resample_device_max_n() else "swap"
+        method = "wide" if n > RESAMPLE_SWAP_MAX_AUTO else "swap"
     if method == "swap":
         _lib.call("cc_resample_device", ctypes.c_uint32(seed), h_begin, h_end, n, m,
                   out.data_ptr() if out.numel() else None, stream_ptr(device))
