@@ -771,8 +771,12 @@ __device__ __forceinline__ void estep_prefetch(const KArgs& a, const State& S, i
 
 // strict-< argmin of NCH aligned chunks (4 slots each, columns col[u] .. col[u] + 3, increasing
 // in u) as a tree (dependency depth 2 + log2 NCH instead of 4 NCH): ties keep the lower slot at
-// every level.
-template <int NCH>
+// every level.  EAGER: the slot indices are materialised as the values are compared and the
+// result is selected without a branch; otherwise the compiler sinks the index selects under the
+// final compare and keeps every compare mask live in SGPR pairs until then.  Same result either
+// way; eager measured C5 275 -> 268 ms and C2 87.1 -> 86.0 ms, C3 (d = 128) unchanged within
+// noise (1649 vs 1652 ms, its SGPR spills 335 -> 287 but no faster), so d = 128 keeps the sunk form.
+template <int NCH, bool EAGER>
 __device__ __forceinline__ void amin_chunks(const float4 (&v)[NCH], const int (&col)[NCH], float& best, int& lab) {
   float bv[NCH];
   int bi[NCH];
@@ -785,18 +789,27 @@ __device__ __forceinline__ void amin_chunks(const float4 (&v)[NCH], const int (&
     if (m1 < m0) { m0 = m1; i0 = i1; }
     bv[u] = m0;
     bi[u] = i0;
+    if constexpr (EAGER) asm volatile("" : "+v"(bi[u]));
   }
 #pragma unroll
   for (int st = 1; st < NCH; st *= 2)
 #pragma unroll
     for (int u = 0; u + st < NCH; u += 2 * st)
       if (bv[u + st] < bv[u]) { bv[u] = bv[u + st]; bi[u] = bi[u + st]; }
-  if (bv[0] < best) { best = bv[0]; lab = bi[0]; }
+  if constexpr (EAGER) {
+    asm volatile("" : "+v"(bi[0]));
+    const bool upd = bv[0] < best;
+    best = upd ? bv[0] : best;
+    lab = upd ? bi[0] : lab;
+  } else if (bv[0] < best) {
+    best = bv[0];
+    lab = bi[0];
+  }
 }
 
 // Lloyd argmin of one half-wave over chunks j0 .. j0 + NCH - 1 (those at or past cnt read the
 // +inf columns CW..CW+3).
-template <int NCH>
+template <int NCH, bool EAGER>
 __device__ __forceinline__ void amin_half(const float* drow, int base, int j0, int cnt, float& best, int& lab) {
   int col[NCH];
   float4 v[NCH];
@@ -809,7 +822,7 @@ __device__ __forceinline__ void amin_half(const float* drow, int base, int j0, i
   // quad for the chunks and serialises their LDS round trips)
 #pragma unroll
   for (int u = 0; u < NCH; ++u) asm volatile("" : "+v"(v[u].x), "+v"(v[u].y), "+v"(v[u].z), "+v"(v[u].w));
-  amin_chunks<NCH>(v, col, best, lab);
+  amin_chunks<NCH, EAGER>(v, col, best, lab);
 }
 
 template <int DP, int NL, int NS>
@@ -861,12 +874,13 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
     float best = INF;
     int lab = 0;
     // wave-uniform (one item per wave): the item's chunk count per half-wave
+    constexpr bool EAGER = DP < 128;
     if (h0 <= 2) {
-      amin_half<2>(drow, base, 0, cnt, best, lab);
+      amin_half<2, EAGER>(drow, base, 0, cnt, best, lab);
     } else if (h0 <= 3) {
-      amin_half<3>(drow, base, 0, cnt, best, lab);
+      amin_half<3, EAGER>(drow, base, 0, cnt, best, lab);
     } else {
-      for (int j0 = 0; j0 < h0; j0 += 4) amin_half<4>(drow, base, j0, cnt, best, lab);  // 4 reads in flight
+      for (int j0 = 0; j0 < h0; j0 += 4) amin_half<4, EAGER>(drow, base, j0, cnt, best, lab);  // 4 reads in flight
     }
     // merge the halves (v_permlane32_swap: lane i <-> i^32 without LDS): lower value, ties to
     // the lower slot (half 0 holds the lower slots)
