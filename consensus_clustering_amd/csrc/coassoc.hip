@@ -534,6 +534,16 @@ __device__ __forceinline__ void expand_chunk_exact_f4(const uint32_t (&w)[32], i
 
 typedef int v8i __attribute__((ext_vector_type(8)));
 
+// One 16-B LDS-DMA piece per lane (global_load_lds_dwordx4: lane l lands at M0 + 16 l), issued
+// from inline asm with the wave-uniform LDS base in M0; completion is awaited explicitly with a
+// vmcnt(0) before the barrier that publishes the data.  No compiler-generated code in these
+// kernels uses M0.
+__device__ __forceinline__ void dma16(const void* g, const void* lds_base) {
+  const unsigned la = static_cast<unsigned>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) const char*)lds_base));
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(__builtin_amdgcn_readfirstlane(la)), "v"(g));
+}
+
 // expansion VALU interleaved per MFMA in the FP4 main loop (power-of-two / exact-K forms)
 #ifndef CO_F4_V
 #define CO_F4_V 10
@@ -804,19 +814,23 @@ __global__ __launch_bounds__(NT, 1) void tiles_kernel(
                                           : (form == BT_PAIR ? bt_pair_bytes(bt_rows) : bt_u16_bytes(bt_rows));
     const int64_t fsrc = form == BT_TRI ? bt_u16_bytes(bt_rows) + bt_pair_bytes(bt_rows)
                                         : (form == BT_PAIR ? bt_u16_bytes(bt_rows) : 0);
+    float* rtab_w = reinterpret_cast<float*>(lds + BT_OFF + fbytes);
+    if (btab) {
+      // the table by LDS-DMA, every 1-KiB piece in flight at once (lane l of wave w copies 16 B
+      // of pieces w, w + 8, ...): the copy loop it replaces waited on each 16-B load before
+      // its LDS store, 4-6 dependent L2 round trips per tile
+      const int vecs = static_cast<int>(fbytes / 16);
+      const char* src = reinterpret_cast<const char*>(btab) + fsrc;
+      for (int pc = wave; pc * 64 < vecs; pc += NW)
+        if (pc * 64 + lane < vecs) dma16(src + (static_cast<int64_t>(pc) * 64 + lane) * 16, lds + BT_OFF + pc * 1024);
+    }
 #pragma unroll
     for (int b = 0; b < NBINS; ++b) hist[b * NT + tid] = 0;
     if (tid <= NBINS) es[tid] = edges[tid];
-    float* rtab_w = reinterpret_cast<float*>(lds + BT_OFF + fbytes);
-    if (btab) {  // 16-B copies (every form is a multiple of 16 B)
-      const int vecs = static_cast<int>(fbytes / 16);
-      const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(btab) + fsrc);
-      uint4* dst = reinterpret_cast<uint4*>(tab);
-      for (int e = tid; e < vecs; e += NT) dst[e] = src[e];
-      if (form != BT_TRI)
-        for (int r = tid; r < bt_rows; r += NT)
-          rtab_w[r] = r > 0 ? 20.0f * __builtin_amdgcn_rcpf(static_cast<float>(r)) : 0.0f;
-    }
+    if (btab && form != BT_TRI)
+      for (int r = tid; r < bt_rows; r += NT)
+        rtab_w[r] = r > 0 ? 20.0f * __builtin_amdgcn_rcpf(static_cast<float>(r)) : 0.0f;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA pieces (opaque to the compiler) landed
     __syncthreads();
     CO_STAMP(st3);
     CO_ACC(2, st2, st3);

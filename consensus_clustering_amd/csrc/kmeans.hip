@@ -157,6 +157,11 @@ struct KArgs {
   int lseg;  // change-list entries per problem and wave segment
 };
 
+// Diagnostics (CCMI_KM_DENSE=1 at launch): every Lloyd item runs the dense M-step, for the
+// sparse-against-dense parity test.  A device global read once per sweep by the scheduling
+// thread, not a KArgs field: a field moved the sweep loops' register allocation (C3 +0.8 %).
+__device__ int cc_km_dense_only = 0;
+
 struct State {
   // unit
   int unit, P;
@@ -1353,7 +1358,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     // ---- sweeps -----------------------------------------------------------------
     for (;;) {
       KM_STAMP(swp);
-      if (tid == 0) schedule(a, S, idx, dist_cost<DP>(), kSparse<DP>);
+      if (tid == 0) schedule(a, S, idx, dist_cost<DP>(), kSparse<DP> && !cc_km_dense_only);
       __syncthreads();
       const int nitems = S.nitems, ncols = S.ncols;
       if (nitems == 0) break;
@@ -2134,6 +2139,19 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
   a.Tws = L.Tws;
   a.seedmax = seedmax;
   a.lsm = (m + 63) & ~63;
+  {
+    static int dense_set = 0;  // the value last written to the device global
+    const char* dm = std::getenv("CCMI_KM_DENSE");
+    const int dense = (dm && dm[0] == '1') ? 1 : 0;
+    if (dense != dense_set) {
+      e = hipMemcpyToSymbolAsync(HIP_SYMBOL(cc_km_dense_only), &dense, sizeof(int), 0, hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) {
+        cc::set_error(std::string("cc_kmeans_batched: ") + hipGetErrorString(e));
+        return CC_ERR_HIP;
+      }
+      dense_set = dense;
+    }
+  }
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nU));
   switch (dpad) {
     case 32: launch<32>(a, blocks, st); break;

@@ -333,3 +333,32 @@ def test_f64_relocation_with_ties_is_pinned():
         differs_from_numpy += not np.array_equal(real.labels_, rule.labels_)
     print(f"f64 relocation with ties: {same_rule}/{len(cases)} identical to sklearn under the lowest-index "
           f"tie rule; numpy's tie order changes sklearn's labels in {differs_from_numpy} of them")
+
+
+def test_sparse_mstep_against_dense(monkeypatch):
+    """The sparse M-step (d = 128: f64 running sums of exact rows updated from change lists)
+    against the dense one (f32 MFMA sums of the 22-bit row image every iteration), on C3-shaped
+    data (d = 128, 8 blobs, K = 2..14, 80 % resamples): the two differ only by rounding, so for
+    K <= k_true every label vector must be identical; above it each engine is checked against
+    sklearn on its own.  Measured (profiles/r04/sparse_dense_r4m.txt, two data seeds): sparse
+    and dense differ in 3 / 52 and 0 / 52 label vectors; each engine has at most one of 52
+    problems that sk_parity cannot explain (a K > k_true problem with >= 99.9 % of its labels
+    equal to sklearn's and an exact inertia within 7e-6 relative of sklearn's), and on the
+    second seed both engines share it, so it is not the sparse M-step's: a known gap of the
+    f32-class engine, allowed once per engine here."""
+    n, d, k_true, Ks, H, seed = 4000, 128, 8, list(range(2, 15)), 4, 3
+    X = blobs(n, d, k_true, seed=11)
+    monkeypatch.delenv("CCMI_KM_DENSE", raising=False)
+    idx, sparse, _, nit_s, st_s = run_gpu(X, Ks, H, 0.8, seed)
+    monkeypatch.setenv("CCMI_KM_DENSE", "1")
+    idx2, dense, _, nit_d, st_d = run_gpu(X, Ks, H, 0.8, seed)
+    assert np.array_equal(idx, idx2)
+    assert st_s[6] > 0 and st_d[6] == 0  # sparse item-sweeps ran in one engine only
+    same = [[np.array_equal(sparse[k, h], dense[k, h]) for h in range(H)] for k in range(len(Ks))]
+    for k, K in enumerate(Ks):
+        if K <= k_true:
+            assert all(same[k]), (K, same[k])
+    ndiff = sum(not v for row in same for v in row)
+    print(f"sparse vs dense M-step: {len(Ks) * H - ndiff}/{len(Ks) * H} label vectors identical")
+    sklearn_parity(X, sparse, idx, Ks, seed, resamples=H, threads=8, max_unexplained=1)
+    sklearn_parity(X, dense, idx, Ks, seed, resamples=H, threads=8, max_unexplained=1)
