@@ -285,6 +285,7 @@ def linkage_raw(D: torch.Tensor, method: str) -> torch.Tensor:
     ws = torch.empty(int(lib.cc_linkage_workspace_bytes(n)), dtype=torch.uint8, device=D.device)
     _lib.call("cc_linkage_nnchain", D.data_ptr(), n, LINKAGE_METHODS[method], Z.data_ptr(), ws.data_ptr(),
               ws.numel(), stream_ptr())
+    _lib.call("cc_linkage_check", ws.data_ptr(), ws.numel(), stream_ptr())
     return Z
 
 
@@ -309,6 +310,7 @@ def linkage_single(D: torch.Tensor) -> np.ndarray:
     out = torch.empty((n - 1, 3), dtype=torch.float64, device=D.device)
     ws = torch.empty(int(_lib.load().cc_linkage_mst_workspace_bytes(n)), dtype=torch.uint8, device=D.device)
     _lib.call("cc_linkage_mst", D.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws.numel(), stream_ptr())
+    _lib.call("cc_linkage_check", ws.data_ptr(), ws.numel(), stream_ptr())
     from .post import single_linkage_finish
 
     return single_linkage_finish(out.cpu().numpy(), n)

@@ -164,8 +164,9 @@ int cc_manhattan(const float* C, int n, int d, double* D, void* stream);
  * sklearn linkage_tree -> scipy.cluster.hierarchy.linkage -> _hierarchy.nn_chain) on the device:
  * D [n][n] float64 symmetric (e.g. from cc_manhattan) is overwritten; Z [n-1][4] float64 receives
  * (x, y, distance, size) per merge in nn_chain's merge order, before linkage()'s stable sort by
- * distance and relabelling (done by the caller).  One workgroup; workspace of
- * cc_linkage_workspace_bytes(n) bytes. */
+ * distance and relabelling (done by the caller).  Runs on G co-resident workgroups joined by
+ * grid barriers (G from n; CCMI_LINK_G overrides, 0 = one workgroup); workspace of
+ * cc_linkage_workspace_bytes(n) bytes; call cc_linkage_check after it. */
 #define CC_LINK_AVERAGE 0
 #define CC_LINK_COMPLETE 1
 #define CC_LINK_WEIGHTED 2
@@ -178,10 +179,16 @@ int cc_linkage_nnchain(double* D, int n, int method, double* Z, void* workspace,
  * _hierarchical_fast.mst_linkage_core, Prim's MST-LINKAGE-CORE) on the device, over the rows of
  * D [n][n] float64 (read only; cc_manhattan's values are DistanceMetric64 cityblock's).
  * out [n-1][3] float64 = (current node, new node, distance) per Prim step; the caller sorts the
- * edges by distance (stable) and labels them (_single_linkage_label).  One workgroup; workspace
- * of cc_linkage_mst_workspace_bytes(n) bytes. */
+ * edges by distance (stable) and labels them (_single_linkage_label).  G co-resident workgroups
+ * as cc_linkage_nnchain; workspace of cc_linkage_mst_workspace_bytes(n) bytes; call
+ * cc_linkage_check after it. */
 size_t cc_linkage_mst_workspace_bytes(int n);
 int cc_linkage_mst(const double* D, int n, double* out, void* workspace, size_t ws_bytes, void* stream);
+
+/* After cc_linkage_nnchain / cc_linkage_mst on `stream` with this workspace: synchronises the
+ * stream and returns CC_ERR_HIP if a grid barrier of the linkage timed out (its output is then
+ * invalid), else CC_OK. */
+int cc_linkage_check(const void* workspace, size_t ws_bytes, void* stream);
 
 /* Batched k-means for every (resample h, K, init) problem, replacing the per-(K, h)
  * clusterer.fit_predict(X[indices]) of CC.py:282 for the default clusterer

@@ -88,6 +88,27 @@ def test_device_mst_equals_oracle(n, seed, ties):
 
     ws = torch.empty(int(_lib.load().cc_linkage_mst_workspace_bytes(n)), dtype=torch.uint8, device="cuda")
     _lib.call("cc_linkage_mst", Dd.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws.numel(), engine.stream_ptr())
+    _lib.call("cc_linkage_check", ws.data_ptr(), ws.numel(), engine.stream_ptr())
+    np.testing.assert_array_equal(out.cpu().numpy(), O.mst_prim(D))
+
+
+@pytest.mark.parametrize("G", [0, 1, 2, 5, 16])
+@pytest.mark.parametrize("n,seed,ties", [(3, 0, True), (257, 1, True), (1500, 2, False), (2000, 3, True)])
+def test_grid_linkage_equals_oracle(G, n, seed, ties, monkeypatch):
+    """The grid forms (G workgroups over index slices, grid barriers; CCMI_LINK_G = 0 is the
+    one-workgroup kernel) give the oracle's nn_chain merges and Prim edges bit for bit, ties
+    included, whatever G (slices of one entry and empty slices included)."""
+    monkeypatch.setenv("CCMI_LINK_G", str(G))
+    D = _distances(n, seed, ties)
+    np.testing.assert_array_equal(engine.linkage_raw(torch.from_numpy(D).cuda(), "average").cpu().numpy(),
+                                  O.nn_chain(D, "average"))
+    from consensus_clustering_amd import _lib
+
+    Dd = torch.from_numpy(D).cuda()
+    out = torch.empty((n - 1, 3), dtype=torch.float64, device="cuda")
+    ws = torch.empty(int(_lib.load().cc_linkage_mst_workspace_bytes(n)), dtype=torch.uint8, device="cuda")
+    _lib.call("cc_linkage_mst", Dd.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws.numel(), engine.stream_ptr())
+    _lib.call("cc_linkage_check", ws.data_ptr(), ws.numel(), engine.stream_ptr())
     np.testing.assert_array_equal(out.cpu().numpy(), O.mst_prim(D))
 
 
