@@ -431,20 +431,25 @@ __device__ __forceinline__ GridWs grid_ws(void* ws) {
 }
 constexpr size_t grid_ws_bytes() { return GHDR + 2 * GMAX * (sizeof(double) + sizeof(int)); }
 
-// Grid barrier: every thread's global writes are complete and written back before the arrival,
-// and every thread reads after the acquire.  Returns false when the wait timed out or another
-// workgroup reported an error (the caller returns at once).
+// Grid barrier.  FULL: every thread's global writes are complete and written back before the
+// arrival and every thread reads after the acquire (agent-scope fences: the D updates of
+// nn_chain cross XCDs).  Light (FULL = false): only the slice minima cross, and they are written
+// and read with agent-scope atomics, so the arrival only has to follow their completion (no
+// cache write-back or invalidation).  Returns false when the wait timed out or another workgroup
+// reported an error (the caller returns at once).
+template <bool FULL>
 __device__ bool grid_sync(const GridWs& gw, unsigned& gen) {
   __shared__ int s_ok;
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores have left
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores and atomics have completed
   __syncthreads();
   if (threadIdx.x == 0) {
     int ok = 1;
     const unsigned want = gen + 1;
-    __threadfence();  // release (writes back this XCD's L2)
+    if constexpr (FULL) __threadfence();  // release (writes back this XCD's L2)
     if (atomicAdd(&gw.bar[0], 1u) == gridDim.x - 1) {
       atomicExch(&gw.bar[0], 0u);
-      __threadfence();
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // the reset is done before the release
+      if constexpr (FULL) __threadfence();
       atomicExch(&gw.bar[1], want);
     } else {
       unsigned polls = 0;
@@ -459,7 +464,7 @@ __device__ bool grid_sync(const GridWs& gw, unsigned& gen) {
         }
       }
     }
-    __threadfence();  // acquire (invalidates this CU's L1 and this XCD's L2)
+    if constexpr (FULL) __threadfence();  // acquire (invalidates this CU's L1 and this XCD's L2)
     s_ok = ok;
   }
   __syncthreads();
@@ -499,16 +504,20 @@ __device__ __forceinline__ void block_argmin_g(double& v, int& i, double* rv, in
 __device__ bool grid_argmin(const GridWs& gw, unsigned& gen, double& v, int& i, double* rv, int* ri) {
   const int par = gen & 1;
   if (threadIdx.x == 0) {
-    gw.pv[par * GMAX + blockIdx.x] = v;
-    gw.pi[par * GMAX + blockIdx.x] = i;
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(gw.pv) + par * GMAX + blockIdx.x,
+                       static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gw.pi + par * GMAX + blockIdx.x, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (!grid_sync(gw, gen)) return false;
+  if (!grid_sync<false>(gw, gen)) return false;
   constexpr double INF = __builtin_huge_val();
   v = INF;
   i = 0x7fffffff;
   if (threadIdx.x < static_cast<int>(gridDim.x)) {  // slice order = index order
-    v = gw.pv[par * GMAX + threadIdx.x];
-    i = gw.pi[par * GMAX + threadIdx.x];
+    v = __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+        reinterpret_cast<unsigned long long*>(gw.pv) + par * GMAX + threadIdx.x, __ATOMIC_RELAXED,
+        __HIP_MEMORY_SCOPE_AGENT)));
+    i = __hip_atomic_load(gw.pi + par * GMAX + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   block_argmin_g(v, i, rv, ri);
   return true;
@@ -632,7 +641,7 @@ __global__ __launch_bounds__(LG) void nnchain_grid_kernel(double* __restrict__ D
         }
       }
     }
-    if (!grid_sync(gw, gen)) return;  // the merged row and column before any later scan
+    if (!grid_sync<true>(gw, gen)) return;  // the merged row and column before any later scan
   }
 }
 
