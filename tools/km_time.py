@@ -25,7 +25,7 @@ m = int(cfg["frac"] * n)
 idx_d = torch.from_numpy(engine.resample_indices(SEED, n, m, 0, H)).to(dev)
 Xd, xn, _, Xhl, e = prepare_rows(X, dev)
 L = engine.new_label_matrix(len(cfg["Ks"]), n, engine.pad_h(H), dev)
-bk = BatchedKMeans(cfg["Ks"], n_init=3, random_state=SEED,
+bk = BatchedKMeans(cfg["Ks"], n_init=3, random_state=SEED, max_iter=int(os.environ.get("KM_MAXITER", 300)),
                    workspace_budget=int(os.environ.get("KM_BUDGET_GB", 8)) << 30)
 ts = []
 for r in range(reps + 1):
