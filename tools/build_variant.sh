@@ -11,6 +11,7 @@ cp -r $REPO/consensus_clustering_amd/csrc $W/consensus_clustering_amd/
 cp $REPO/include/ccmi.h $W/include/
 cp "$SRC" $W/consensus_clustering_amd/csrc/kmeans.hip
 [ -n "$CO_SRC" ] && cp "$CO_SRC" $W/consensus_clustering_amd/csrc/coassoc.hip  # a coassoc.hip variant (with REBUILD=coassoc)
+[ -n "$PR_SRC" ] && cp "$PR_SRC" $W/consensus_clustering_amd/csrc/predict.hip  # a predict.hip variant (with REBUILD=predict)
 mkdir -p $W/build
 cp $REPO/build/ccmi/*.o $W/build/ 2>/dev/null || true  # unchanged objects are reused (kmeans.o rebuilds)
 for o in kmeans $REBUILD; do rm -f $W/build/$o.o; done  # REBUILD="coassoc ...": objects whose flags change
