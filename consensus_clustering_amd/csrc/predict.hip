@@ -40,8 +40,8 @@ __global__ __launch_bounds__(256) void manhattan_kernel(const float* __restrict_
     ++bi;
   }
   const int bj = bi + t;
-  __shared__ __attribute__((aligned(16))) float sa[KS][TB];
-  __shared__ __attribute__((aligned(16))) float sb[KS][TB];
+  __shared__ __attribute__((aligned(16))) double sa[KS][TB];  // staged as float64: no conversions in the k loop
+  __shared__ __attribute__((aligned(16))) double sb[KS][TB];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const int i0 = bi * TB, j0 = bj * TB;
   double acc[RB][RB];
@@ -98,19 +98,23 @@ __global__ __launch_bounds__(256) void manhattan_kernel(const float* __restrict_
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        sa[sk + q][sr + 64 * h] = (&ga[h].x)[q];
-        sb[sk + q][sr + 64 * h] = (&gb[h].x)[q];
+        sa[sk + q][sr + 64 * h] = static_cast<double>((&ga[h].x)[q]);
+        sb[sk + q][sr + 64 * h] = static_cast<double>((&gb[h].x)[q]);
       }
     __syncthreads();
     if (k0 + KS < d) load_any(k0 + KS);  // in flight under this slab
     const int kn = min(KS, d - k0);
     for (int k = 0; k < kn; ++k) {
-      const float4 a0 = *reinterpret_cast<const float4*>(&sa[k][RB * ty]);
-      const float4 a1 = *reinterpret_cast<const float4*>(&sa[k][RB * ty + 4]);
-      const float4 b0 = *reinterpret_cast<const float4*>(&sb[k][RB * tx]);
-      const float4 b1 = *reinterpret_cast<const float4*>(&sb[k][RB * tx + 4]);
-      const double a[RB] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const double b[RB] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      double a[RB], b[RB];
+#pragma unroll
+      for (int q = 0; q < RB; q += 2) {
+        const double2 av = *reinterpret_cast<const double2*>(&sa[k][RB * ty + q]);
+        const double2 bv = *reinterpret_cast<const double2*>(&sb[k][RB * tx + q]);
+        a[q] = av.x;
+        a[q + 1] = av.y;
+        b[q] = bv.x;
+        b[q + 1] = bv.y;
+      }
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
