@@ -82,6 +82,22 @@ constexpr int TMAX = 6;             // max local trials: 2 + floor(ln 127)
 constexpr int KMAX = 127;
 constexpr int DSD = CW + 4;         // distance-tile row stride (floats): 16-B rows, conflict-free b128
 constexpr int NRING = 4;            // X tile ring: t+1 (gather), t (dist), t-2 (M-step)
+// Pair mode (d <= 64, sweeps of at most 4 slot tiles = 128 slots): each barrier interval moves
+// two row tiles (2p, 2p+1) through every stage, sequentially on the same waves, so the narrow
+// sweeps at the end of a unit pay half the barriers and twice the work per wave chain.  Row
+// tile 2p+1's distances sit in the same distance buffer at column offset 128 (the +inf chunk at
+// CW stays shared), the ring holds 8 tiles and the label buffers 4.  Every row's arithmetic,
+// every item's wave and every accumulation order are those of the one-tile loop, so the
+// results are identical.
+#ifndef KM_PAIR
+#define KM_PAIR 1
+#endif
+template <int DP>
+constexpr bool kPair = KM_PAIR && DP <= 64;
+template <int DP>
+constexpr int kRing = kPair<DP> ? 8 : NRING;
+template <int DP>
+constexpr int kLsb = kPair<DP> ? 4 : 2;  // label buffers of the E-step -> M-step hand-off
 constexpr int US = CC_KM_USTRIDE;
 // step-dealing cost units (a Lloyd step of K = 20 costs 80, a seeding step 20): the distance
 // MFMAs and the M-step of a wave's own slots, measured in the same units from the phase stamps
@@ -205,14 +221,14 @@ template <int DP>
 struct Lay {
   static constexpr int IMG = RT * DP * 2;     // one f16 image (hi or lo) of a tile, bytes
   static constexpr int SLOT = 2 * IMG;        // ring slot: hi image then lo image
-  static constexpr int OFF_D = NRING * SLOT;  // distance tiles [2][RT][DSD] f32
+  static constexpr int OFF_D = kRing<DP> * SLOT;  // distance tiles [2][RT][DSD] f32
   static constexpr int DBUF = RT * DSD * 4;
   static constexpr int U_END = OFF_D + 2 * DBUF;
   static constexpr int S_BYTES = CW * DP * 4;  // centre sums [CW][DP] f32, aliasing ring + D
   static_assert(S_BYTES <= U_END, "centre sums must fit in the ring + distance tiles");
   static constexpr int OFF_LS = (U_END + 32 + 15) / 16 * 16;  // labels [2][IMAX][RT] u8 (32 B slack: E-step over-reads)
-  static constexpr int OFF_XN = OFF_LS + 2 * IMAX * RT;  // row norms [NRING][64] f32 (DMA'd, 32 used)
-  static constexpr int OFF_ST = OFF_XN + NRING * 64 * 4;
+  static constexpr int OFF_XN = OFF_LS + kLsb<DP> * IMAX * RT;  // row norms [kRing][64] f32 (DMA'd, 32 used)
+  static constexpr int OFF_ST = OFF_XN + kRing<DP> * 64 * 4;
   static constexpr int TOTAL = OFF_ST + ((sizeof(State) + 15) / 16) * 16;
   static_assert(TOTAL <= 163840, "LDS budget");
   static_assert(NSS % 4 == 0 && (NSS_D < 4 || NSS_D % 4 == 0), "seeding steps are read in batches");
@@ -830,7 +846,7 @@ __device__ __forceinline__ void amin_half(const float* drow, int base, int j0, i
   amin_chunks<NCH, EAGER>(v, col, best, lab);
 }
 
-template <int DP, int NL, int NS>
+template <int DP, int NL, int NS, bool PM = false>
 __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int T, int tidl, const float* Dt,
                                       uint8_t* Ls, const float* XN, uint8_t* glab, float* dbuf,
                                       const unsigned (&pre)[NS], const unsigned (&lw)[NL], int nl, int ns,
@@ -842,9 +858,12 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
   const int w = (tidl >> 6) & 7, hh = (tidl >> 5) & 1;
   const int erow = te * RT + ler;
   const bool eok = erow < m;
-  const float* drow = Dt + (te & 1) * (RT * DSD) + ler * DSD;
-  uint8_t* lsb = Ls + (te & 1) * (IMAX * RT);
-  const float xnr = XN[(te % NRING) * 64 + ler];
+  // pair mode: tile te's distances in buffer (te >> 1) & 1 at column offset 128 (te & 1), its
+  // labels in buffer te & 3
+  const int coff = PM ? 128 * (te & 1) : 0;
+  const float* drow = Dt + (PM ? ((te >> 1) & 1) : (te & 1)) * (RT * DSD) + ler * DSD;
+  uint8_t* lsb = Ls + (PM ? (te & 3) : (te & 1)) * (IMAX * RT);
+  const float xnr = XN[(te % kRing<DP>) * 64 + ler];
   constexpr float INF = __builtin_huge_valf();
   // seeding steps first (one item per half-wave): descriptors and distances of every step in
   // flight together, then min with the closest distance, store for the potential and the next
@@ -858,7 +877,10 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
 #pragma unroll
     for (int i = 0; i < B; ++i) d[i] = *reinterpret_cast<const int2*>(&S.sdesc[w][i0 + i][hh].z);
 #pragma unroll
-    for (int i = 0; i < B; ++i) dd[i] = drow[d[i].y & 0xFFFF];
+    for (int i = 0; i < B; ++i) {
+      const int col = d[i].y & 0xFFFF;
+      dd[i] = drow[(PM && col != CW) ? col + coff : col];
+    }
 #pragma unroll
     for (int i = 0; i < B; ++i) {
       const float dist = fmaxf(xnr + dd[i], 0.f);
@@ -875,7 +897,7 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
     if (i >= nl) break;
     const unsigned ww = lw[i];
     const int off = iw_off(ww), C = (iw_K(ww) + 3) >> 2, h0 = (C + 1) >> 1;
-    const int base = off + (hh ? 4 * h0 : 0), cnt = hh ? C - h0 : h0;
+    const int base = off + coff + (hh ? 4 * h0 : 0), cnt = hh ? C - h0 : h0;
     float best = INF;
     int lab = 0;
     // wave-uniform (one item per wave): the item's chunk count per half-wave
@@ -897,7 +919,7 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
       best = ob;
       lab = ol;
     }
-    lab -= off;
+    lab -= off + coff;
     if (hh == 0) {
       if (eok) {
         glab[(static_cast<size_t>(2 * iw_prob(ww) + iw_buf(ww))) * a.lsm + erow] = static_cast<uint8_t>(lab);
@@ -1358,7 +1380,15 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
     // ---- sweeps -----------------------------------------------------------------
     for (;;) {
       KM_STAMP(swp);
-      if (tid == 0) schedule(a, S, idx, dist_cost<DP>(), kSparse<DP> && !cc_km_dense_only);
+      if (tid == 0) {
+        // d <= 64 (pair mode): the larger kernel body would leave these helpers out of line and
+        // the KArgs copied to scratch; inline them there (at d = 128 the default choice stands)
+        if constexpr (kPair<DP>) {
+          [[clang::always_inline]] schedule(a, S, idx, dist_cost<DP>(), kSparse<DP> && !cc_km_dense_only);
+        } else {
+          schedule(a, S, idx, dist_cost<DP>(), kSparse<DP> && !cc_km_dense_only);
+        }
+      }
       __syncthreads();
       const int nitems = S.nitems, ncols = S.ncols;
       if (nitems == 0) break;
@@ -1375,6 +1405,8 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         S.sdesc[w][i][h] = seed_desc(a, S, S.sstep[w][i][h], T1);
       }
       const int hh = lane >> 5, lr = lane & 31;
+      const bool pm = kPair<DP> && ncols <= 4 * 32;  // block-uniform
+      const int TP = (T + 1) >> 1;                    // row-tile pairs (pair mode)
 #ifdef CC_KM_STAMPS
       unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1404,6 +1436,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         unsigned pre[NSS_D];
 #pragma unroll
         for (int i = 0; i < NSS_D; ++i) pre[i] = 0;
+        if (!pm) {
         // pipeline prologue: tile 0 in the ring, indices of tile 1
         TileIdx<DP> nI;
         {
@@ -1422,7 +1455,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         for (int t = 0; t <= T + 1; ++t) {
           KM_STAMP(s0);
           if (t < T) {  // distances of tile t (MFMA) -> D[t & 1]
-            const char* xs = ring + (t % NRING) * LY::SLOT;
+            const char* xs = ring + (t % kRing<DP>) * LY::SLOT;
             float* dtile = Dt + (t & 1) * (RT * DSD);
             if (nsub == 2)
               dist_tiles<DP, 2>(a, S, xs, dtile, wave, lane, ah0, al0, ah1, al1);
@@ -1439,7 +1472,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           TileAddr<DP> An;
           tile_addr<DP>(a, nI, wave, lane, An);
           idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
-          if (t + 1 < T) tile_issue<DP>(An, ring + ((t + 1) % NRING) * LY::SLOT, XN + ((t + 1) % NRING) * 64, wave);
+          if (t + 1 < T) tile_issue<DP>(An, ring + ((t + 1) % kRing<DP>) * LY::SLOT, XN + ((t + 1) % kRing<DP>) * 64, wave);
           KM_STAMP(s2);
           {
             int tidl = tid;
@@ -1462,6 +1495,68 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           KM_ACC(2, s2, s2e);
           KM_ACC(4, s2e, s3);
           KM_ACC(5, s3, s4);
+        }
+        } else if constexpr (kPair<DP>) {
+          // pair mode: prologue tiles 0, 1 in the ring, indices of tiles 2, 3; per interval the
+          // distances of tiles 2p, 2p+1 (this wave's one slot tile, A fragments shared), the
+          // gather of 2p+2, 2p+3, the E-step share of 2p-2, 2p-1
+          TileIdx<DP> nI0, nI1;
+          unsigned preB[NSS_D];
+#pragma unroll
+          for (int i = 0; i < NSS_D; ++i) preB[i] = 0;
+          {
+            TileIdx<DP> I0, I1;
+            TileAddr<DP> A0, A1;
+            idx_issue<DP>(a, idx, 0, wave, lane, I0);
+            idx_issue<DP>(a, idx, RT, wave, lane, I1);
+            tile_addr<DP>(a, I0, wave, lane, A0);
+            tile_addr<DP>(a, I1, wave, lane, A1);
+            tile_issue<DP>(A0, ring, XN, wave);
+            if (T > 1) tile_issue<DP>(A1, ring + LY::SLOT, XN + 64, wave);
+            idx_issue<DP>(a, idx, 2 * RT, wave, lane, nI0);
+            idx_issue<DP>(a, idx, 3 * RT, wave, lane, nI1);
+            dma_wait();
+            tile_addr_hold<DP>(A0);
+            tile_addr_hold<DP>(A1);
+          }
+          __syncthreads();
+          for (int pr = 0; pr <= TP + 1; ++pr) {
+            const int tA = 2 * pr, tB = tA + 1;
+            if (nsub == 1) {
+              float* dtile = Dt + (pr & 1) * (RT * DSD);
+              if (tA < T) dist_tiles<DP, 1>(a, S, ring + (tA % kRing<DP>) * LY::SLOT, dtile, wave, lane, ah0, al0, ah1, al1);
+              if (tB < T) dist_tiles<DP, 1>(a, S, ring + (tB % kRing<DP>) * LY::SLOT, dtile + 128, wave, lane, ah0, al0, ah1, al1);
+            }
+            TileAddr<DP> An0, An1;
+            tile_addr<DP>(a, nI0, wave, lane, An0);
+            tile_addr<DP>(a, nI1, wave, lane, An1);
+            idx_issue<DP>(a, idx, (tA + 4) * RT, wave, lane, nI0);
+            idx_issue<DP>(a, idx, (tA + 5) * RT, wave, lane, nI1);
+            if (tA + 2 < T)
+              tile_issue<DP>(An0, ring + ((tA + 2) % kRing<DP>) * LY::SLOT, XN + ((tA + 2) % kRing<DP>) * 64, wave);
+            if (tB + 2 < T)
+              tile_issue<DP>(An1, ring + ((tB + 2) % kRing<DP>) * LY::SLOT, XN + ((tB + 2) % kRing<DP>) * 64, wave);
+            {
+              int tidl = tid;
+              asm volatile("" : "+v"(tidl));
+              unsigned npre[NSS_D], npreB[NSS_D];
+              estep_prefetch<NSS_D>(a, S, tA, T, tidl, ns, dbuf, npre);
+              estep_prefetch<NSS_D>(a, S, tB, T, tidl, ns, dbuf, npreB);
+              estep<DP, NLS_D, NSS_D, true>(a, S, tA - 1, T, tidl, Dt, Ls, XN, glab, dbuf, pre, lw, nl, ns, es);
+              if (((tA - 1) % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
+              estep<DP, NLS_D, NSS_D, true>(a, S, tA, T, tidl, Dt, Ls, XN, glab, dbuf, preB, lw, nl, ns, es);
+              if ((tA % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
+#pragma unroll
+              for (int i = 0; i < NSS_D; ++i) {
+                pre[i] = npre[i];
+                preB[i] = npreB[i];
+              }
+            }
+            dma_wait();  // tiles 2p+2, 2p+3 and the indices of 2p+4, 2p+5 have landed
+            tile_addr_hold<DP>(An0);
+            tile_addr_hold<DP>(An1);
+            __syncthreads();
+          }
         }
         estep_flush(S, tid, es);
       } else {
@@ -1502,6 +1597,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         __syncthreads();
         KM_STAMP(sw0);
         KM_ACC(6, swp, sw0);
+        if (!pm) {
         for (int t = 0; t <= T + 1; ++t) {
           KM_STAMP(s0);
           int tidl = tid;
@@ -1515,7 +1611,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           // M-steps of tile t-2 (one-hot x X on f16 MFMA; counts by popcount)
           if (t >= 2) {
             const int tm = t - 2;
-            const char* xs = ring + (tm % NRING) * LY::SLOT;
+            const char* xs = ring + (tm % kRing<DP>) * LY::SLOT;
             const uint8_t* lsb = Ls + (tm & 1) * (IMAX * RT);
             if (mact0 || mact1)  // both tiles share the transposed X reads (a tile without running
                                  // centres has an all-zero one-hot)
@@ -1531,6 +1627,40 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           KM_ACC(2, s1, s2);
           KM_ACC(3, s2, s3);
           KM_ACC(5, s3, s4);
+        }
+        } else if constexpr (kPair<DP>) {
+          // pair mode: per interval the E-steps of tiles 2p-2, 2p-1 and the M-steps of 2p-4,
+          // 2p-3, in tile order
+          unsigned preB[NSS];
+#pragma unroll
+          for (int i = 0; i < NSS; ++i) preB[i] = 0;
+          for (int pr = 0; pr <= TP + 1; ++pr) {
+            const int tA = 2 * pr, tB = tA + 1;
+            int tidl = tid;
+            asm volatile("" : "+v"(tidl));
+            unsigned npre[NSS], npreB[NSS];
+            estep_prefetch<NSS>(a, S, tA, T, tidl, ns, dbuf, npre);
+            estep_prefetch<NSS>(a, S, tB, T, tidl, ns, dbuf, npreB);
+            estep<DP, NLS, NSS, true>(a, S, tA - 1, T, tidl, Dt, Ls, XN, glab, dbuf, pre, lw, nl, ns, es);
+            if (((tA - 1) % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
+            estep<DP, NLS, NSS, true>(a, S, tA, T, tidl, Dt, Ls, XN, glab, dbuf, preB, lw, nl, ns, es);
+            if ((tA % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+              const int tm = tA - 4 + g;
+              if (tm >= 0 && tm < T && (mact0 || mact1)) {
+                const char* xs = ring + (tm % kRing<DP>) * LY::SLOT;
+                const uint8_t* lsb = Ls + (tm & 3) * (IMAX * RT);
+                mstep_tiles<DP, 2>(xs, lsb + myit0 * RT, lsb + myit1 * RT, lane, mycl0, mycl1, sacc0, sacc1, mcnt0, mcnt1, mact1);
+              }
+            }
+#pragma unroll
+            for (int i = 0; i < NSS; ++i) {
+              pre[i] = npre[i];
+              preB[i] = npreB[i];
+            }
+            __syncthreads();
+          }
         }
         estep_flush(S, tid, es);
         dma_wait();  // label and closest-distance stores land before the post-sweep reads
@@ -1596,7 +1726,11 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           if (!S.need_sel[p]) continue;
           if ((j++ % NW) != wave) continue;
           const int ss = S.sslot[p];
-          kpp_select(a, S, p, dbuf + (static_cast<size_t>(ss) * T1 + S.cs[p]) * a.lsm, lane);
+          if constexpr (kPair<DP>) {
+            [[clang::always_inline]] kpp_select(a, S, p, dbuf + (static_cast<size_t>(ss) * T1 + S.cs[p]) * a.lsm, lane);
+          } else {
+            kpp_select(a, S, p, dbuf + (static_cast<size_t>(ss) * T1 + S.cs[p]) * a.lsm, lane);
+          }
         }
       }
       // initial centres of problems leaving seeding: the chosen rows (exact f32)
@@ -1729,8 +1863,13 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           if (S.ikind[it] != IK_RUN) continue;
           const int p = S.iprob[it];
           if (S.nempty[p] == 0) continue;
-          relocate<DP>(a, idx, p, S.ioff[it], cen, Sm, S, glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm,
-                       rdist, tid);
+          if constexpr (kPair<DP>) {
+            [[clang::always_inline]] relocate<DP>(a, idx, p, S.ioff[it], cen, Sm, S,
+                                                  glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm, rdist, tid);
+          } else {
+            relocate<DP>(a, idx, p, S.ioff[it], cen, Sm, S, glab + static_cast<size_t>(2 * p + S.lcur[p]) * a.lsm,
+                         rdist, tid);
+          }
           __syncthreads();
         }
       }
