@@ -208,39 +208,83 @@ struct WG {
   uint8_t* lbest;
 };
 
-constexpr int G = 4;  // centres per E-step pass (independent FMA chains per thread)
 
 // The unit's centred row r (materialised: X[idx[r]][k] - mean[k], rounded once).
 __device__ __forceinline__ const double* xrow(const WG& w, int d, int r) { return w.xc + static_cast<size_t>(r) * d; }
 
-// The E-step argmin of row x over the K centres (|c|^2 in cn): G centres per pass, each
-// |c_j|^2 - 2 x.c_j with x.c_j the sequential FMA chain of dotc; strict < over increasing j.
-__device__ __forceinline__ int estep_row(const double* x, const double* cen, const double* cn, int K, int d) {
-  double best = 0.0;
-  int lab = 0;
-  for (int j0 = 0; j0 < K; j0 += G) {
-    double acc[G];
+// The E-step argmin of every row over the K centres: |c_j|^2 - 2 x.c_j with x.c_j the sequential
+// FMA chain over k = 0 .. d-1 (the small-matrix dgemm order), strict < over increasing j.  Thread
+// t takes row r0 + t of each block of NT rows and EG centres per pass as EG accumulators; the
+// block's rows are staged in LDS EKC features at a time (coalesced loads, issued one chunk ahead),
+// the centres' features beside them (read as broadcasts).  Round 4: it replaced a per-thread row
+// loop over global memory (4 centres per pass, uncoalesced row reads); same labels.
+constexpr int EG = 16;   // centres per pass
+constexpr int EKC = 8;   // features per staged chunk
+constexpr int EXS = EKC + 1;  // staged row stride (doubles): 2-way bank conflicts at most
+__device__ __noinline__ void estep_block(const WG& w, const double* cen, const double* cn, int K, int d, int m,
+                                         double* xs, double* cs, int tid) {
+  const int nkc = (d + EKC - 1) / EKC;  // chunks per pass
+  const int npass = (K + EG - 1) / EG;
+  for (int r0 = 0; r0 < m; r0 += NT) {
+    const int nrows = m - r0 < NT ? m - r0 : NT;
+    // the block's rows for chunk c = pass * nkc + kc, loaded into registers one chunk ahead of
+    // its FMAs (all EKC loads of a thread in flight together)
+    double v[EKC];
+    auto load = [&](int c) __attribute__((always_inline)) {
+      const int k0 = (c % nkc) * EKC;
+      const int kc = d - k0 < EKC ? d - k0 : EKC;
 #pragma unroll
-    for (int g = 0; g < G; ++g) acc[g] = 0.0;
-    const int ng = K - j0 < G ? K - j0 : G;
-    for (int k = 0; k < d; ++k) {
-      const double xk = x[k];
+      for (int i = 0; i < EKC; ++i) {
+        const int e = tid + NT * i, rr = e / EKC, kk = e - rr * EKC;
+        v[i] = (rr < nrows && kk < kc) ? xrow(w, d, r0 + rr)[k0 + kk] : 0.0;
+      }
+    };
+    load(0);
+    double best = 0.0;
+    int lab = 0;
+    for (int pass = 0; pass < npass; ++pass) {
+      const int j0 = pass * EG;
+      const int ng = K - j0 < EG ? K - j0 : EG;
+      double acc[EG];
 #pragma unroll
-      for (int g = 0; g < G; ++g)
-        if (g < ng) acc[g] = __fma_rn(xk, cen[static_cast<size_t>(j0 + g) * d + k], acc[g]);
-    }
+      for (int g = 0; g < EG; ++g) acc[g] = 0.0;
+      for (int kc0 = 0; kc0 < nkc; ++kc0) {
+        const int k0 = kc0 * EKC;
+        const int kc = d - k0 < EKC ? d - k0 : EKC;
+        __syncthreads();  // the previous chunk has been consumed
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (g >= ng) break;
-      const int j = j0 + g;
-      const double dj = __fma_rn(-2.0, acc[g], cn[j]);
-      if (j == 0 || dj < best) {
-        best = dj;
-        lab = j;
+        for (int i = 0; i < EKC; ++i) {
+          const int e = tid + NT * i, rr = e / EKC, kk = e - rr * EKC;
+          xs[rr * EXS + kk] = v[i];
+        }
+        for (int e = tid; e < EKC * EG; e += NT) {
+          const int kk = e / EG, g = e - kk * EG;
+          cs[e] = (kk < kc && g < ng) ? cen[static_cast<size_t>(j0 + g) * d + k0 + kk] : 0.0;
+        }
+        __syncthreads();
+        const int c = pass * nkc + kc0;
+        if (c + 1 < npass * nkc) load(c + 1);  // in flight under this chunk's FMAs
+        for (int kk = 0; kk < kc; ++kk) {
+          const double xk = xs[tid * EXS + kk];
+#pragma unroll
+          for (int g = 0; g < EG; ++g)
+            if (g < ng) acc[g] = __fma_rn(xk, cs[kk * EG + g], acc[g]);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < EG; ++g) {
+        if (g >= ng) break;
+        const int j = j0 + g;
+        const double dj = __fma_rn(-2.0, acc[g], cn[j]);
+        if (j == 0 || dj < best) {
+          best = dj;
+          lab = j;
+        }
       }
     }
+    if (tid < nrows) w.lab[r0 + tid] = lab;
   }
-  return lab;
+  __syncthreads();
 }
 
 // centred feature k of resample row r
@@ -255,6 +299,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
   __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[TMAX], s_map[KMAX + 1];
   __shared__ double s_pot[TMAX], s_tol, s_red[NT];
   __shared__ int s_ired[NT];
+  __shared__ double s_xs[NT * EXS], s_cs[EKC * EG];  // estep_block staging
   const int tid = threadIdx.x;
   char* base = a.ws + static_cast<size_t>(blockIdx.x) * a.per_wg;
   WG w;
@@ -406,9 +451,9 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
         int chg = 0;
         for (int j = tid; j < K; j += NT) s_ired[j] = 0;
         __syncthreads();
+        estep_block(w, cen, s_red, K, d, m, s_xs, s_cs, tid);
         for (int r = tid; r < m; r += NT) {
-          const int lab = estep_row(xrow(w, d, r), cen, s_red, K, d);
-          w.lab[r] = lab;
+          const int lab = w.lab[r];  // written by this thread in estep_block
           chg |= (lab != w.lold[r]);
           atomicAdd(&s_ired[lab], 1);  // counts (integers: order-free)
         }
@@ -576,8 +621,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
           s_red[j] = einsum_sq([&](int k) { return cj[k]; }, d);
         }
         __syncthreads();
-        for (int r = tid; r < m; r += NT) w.lab[r] = estep_row(xrow(w, d, r), cen, s_red, K, d);
-        __syncthreads();
+        estep_block(w, cen, s_red, K, d, m, s_xs, s_cs, tid);
       }
       // inertia: per-row squared distance to its centre, summed in row order
       for (int r = tid; r < m; r += NT) {
