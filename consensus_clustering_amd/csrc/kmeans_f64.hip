@@ -31,6 +31,9 @@
 // per (cluster, feature) with coalesced row reads instead of one thread per feature
 // read-modify-writing global sums row after row.  Every value keeps its sequential order, so
 // the results are bit-identical to the previous kernel (and to sklearn where it was).
+// The E-step and the k-means++ distances run on the float64 matrix cores (v_mfma_f64_16x16x4_f64,
+// whose per-output accumulation is the sequential FMA chain: see mfma_dots), 16 rows x 16 centres
+// per instruction, the operands read straight from the row-major centred rows.
 #include <hip/hip_runtime.h>
 #include <cstring>
 
@@ -202,6 +205,22 @@ __device__ double blas_gemv_t_ones(const double* x, int m, int col, int ncol) {
   return y;
 }
 
+// Diagnostic build only (-DCC_F64_STAMPS, tools/f64_stamps.py): thread 0's wall-clock split of
+// the units' phases.
+#ifdef CC_F64_STAMPS
+__device__ unsigned long long cc_f64_stamps[16];
+#define F64_STAMP(ph)                               \
+  do {                                              \
+    if (tid == 0) {                                 \
+      const unsigned long long t_ = wall_clock64(); \
+      st_acc[ph] += t_ - st_t;                      \
+      st_t = t_;                                    \
+    }                                               \
+  } while (0)
+#else
+#define F64_STAMP(ph)
+#endif
+
 struct WG {
   double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew, *xc;
   int32_t *lab, *lold, *ord;
@@ -212,77 +231,172 @@ struct WG {
 // The unit's centred row r (materialised: X[idx[r]][k] - mean[k], rounded once).
 __device__ __forceinline__ const double* xrow(const WG& w, int d, int r) { return w.xc + static_cast<size_t>(r) * d; }
 
-// The E-step argmin of every row over the K centres: |c_j|^2 - 2 x.c_j with x.c_j the sequential
-// FMA chain over k = 0 .. d-1 (the small-matrix dgemm order), strict < over increasing j.  Thread
-// t takes row r0 + t of each block of NT rows and EG centres per pass as EG accumulators; the
-// block's rows are staged in LDS EKC features at a time (coalesced loads, issued one chunk ahead),
-// the centres' features beside them (read as broadcasts).  Round 4: it replaced a per-thread row
-// loop over global memory (4 centres per pass, uncoalesced row reads); same labels.
-constexpr int EG = 16;   // centres per pass
-constexpr int EKC = 8;   // features per staged chunk
-constexpr int EXS = EKC + 1;  // staged row stride (doubles): 2-way bank conflicts at most
-__device__ __noinline__ void estep_block(const WG& w, const double* cen, const double* cn, int K, int d, int m,
-                                         double* xs, double* cs, int tid) {
-  const int nkc = (d + EKC - 1) / EKC;  // chunks per pass
-  const int npass = (K + EG - 1) / EG;
-  for (int r0 = 0; r0 < m; r0 += NT) {
-    const int nrows = m - r0 < NT ? m - r0 : NT;
-    // the block's rows for chunk c = pass * nkc + kc, loaded into registers one chunk ahead of
-    // its FMAs (all EKC loads of a thread in flight together)
-    double v[EKC];
-    auto load = [&](int c) __attribute__((always_inline)) {
-      const int k0 = (c % nkc) * EKC;
-      const int kc = d - k0 < EKC ? d - k0 : EKC;
+// ---- float64 dot products on the matrix cores -------------------------------------------------
+// v_mfma_f64_16x16x4_f64 accumulates each of its outputs as the sequential fused multiply-add
+// chain over its 4 k values, starting from C: measured bit-identical to the VALU chain
+// fma(a3, b3, fma(a2, b2, fma(a1, b1, fma(a0, b0, c)))) on 2^20 mixed-exponent results
+// (tools/mfma_f64_probe.hip, profiles/r04/mfma_f64_probe.txt).  A chain of them over k-steps
+// 0 .. d/4-1 is therefore the same sequential FMA dot product (the small-matrix dgemm order) the
+// VALU loops computed, 1024 FMAs per instruction, its operands read straight from the row-major
+// rows (lane l: row l & 15, feature 4s + (l >> 4); consecutive steps reuse the same cache lines).
+// Orientation: A = 16 "centres", B = 16 rows; D's lane l holds row l & 15 against centres
+// (l >> 4) + 4i, i = 0..3.  Features past d (d % 4 != 0) enter as exact zeros in both operands:
+// fma(0, 0, acc) = acc for the accumulators here (never -0: they start at +0).
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+constexpr int MG = 4;  // k-steps per operand load group; two groups in flight
+
+template <int RT, int CT>
+__device__ __forceinline__ void mfma_dots(const double* const (&pa)[CT], const double* const (&pb)[RT], int d,
+                                          int q, f64x4 (&acc)[RT][CT]) {
 #pragma unroll
-      for (int i = 0; i < EKC; ++i) {
-        const int e = tid + NT * i, rr = e / EKC, kk = e - rr * EKC;
-        v[i] = (rr < nrows && kk < kc) ? xrow(w, d, r0 + rr)[k0 + kk] : 0.0;
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const int S = d >> 2;
+  double a0[MG][CT], b0[MG][RT], a1[MG][CT], b1[MG][RT];
+  auto ld = [&](double (&a)[MG][CT], double (&b)[MG][RT], int s0) __attribute__((always_inline)) {
+    if (s0 >= S) return;
+#pragma unroll
+    for (int i = 0; i < MG; ++i) {
+      const int s = s0 + i < S ? s0 + i : S - 1;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) a[i][ct] = pa[ct][4 * s];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) b[i][rt] = pb[rt][4 * s];
+    }
+  };
+  auto mm = [&](const double (&a)[MG][CT], const double (&b)[MG][RT], int s0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < MG; ++i)
+      if (s0 + i < S)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+            acc[rt][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i][ct], b[i][rt], acc[rt][ct], 0, 0, 0);
+  };
+  ld(a0, b0, 0);
+  for (int s0 = 0; s0 < S; s0 += 2 * MG) {
+    ld(a1, b1, s0 + MG);
+    mm(a0, b0, s0);
+    ld(a0, b0, s0 + 2 * MG);
+    mm(a1, b1, s0 + MG);
+  }
+  if (d & 3) {  // the last, partial k-step
+    const bool in = 4 * S + q < d;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const double bv = in ? pb[rt][4 * S] : 0.0;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        acc[rt][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? pa[ct][4 * S] : 0.0, bv, acc[rt][ct], 0, 0, 0);
+    }
+  }
+}
+
+// (value, index) lexicographic minimum: with the centres visited in increasing index it is the
+// sequential scan's strict-< argmin (lowest index on ties)
+__device__ __forceinline__ void lexmin(double& v, int& j, double v2, int j2) {
+  if (v2 < v || (v2 == v && j2 < j)) {
+    v = v2;
+    j = j2;
+  }
+}
+
+// The E-step argmin of every row over the K centres: |c_j|^2 - 2 x.c_j (one rounding, as
+// sklearn's dgemm with beta = 1 on the centre norms), strict < over increasing j.  Each wave takes
+// RT row tiles of 16 at a time and the centres 16 * CT per pass; the running (distance, label) of
+// its rows stays in registers across passes.
+template <int RT, int CT>
+__device__ void estep_tiles(const WG& w, const double* cen, const double* cn, int K, int d, int m, int tid) {
+  const int l = tid & 63, q = l >> 4, c16 = l & 15;
+  const int ntile = (m + 15) >> 4;
+  for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
+    const double* pb[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int r = (t0 + rt) * 16 + c16;
+      pb[rt] = w.xc + static_cast<size_t>(r < m ? r : m - 1) * d + q;
+    }
+    double bv[RT];
+    int bj[RT];
+    for (int j0 = 0; j0 < K; j0 += 16 * CT) {
+      const double* pa[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int j = j0 + 16 * ct + c16;
+        pa[ct] = cen + static_cast<size_t>(j < K ? j : K - 1) * d + q;
       }
-    };
-    load(0);
-    double best = 0.0;
-    int lab = 0;
-    for (int pass = 0; pass < npass; ++pass) {
-      const int j0 = pass * EG;
-      const int ng = K - j0 < EG ? K - j0 : EG;
-      double acc[EG];
+      f64x4 acc[RT][CT];
+      mfma_dots<RT, CT>(pa, pb, d, q, acc);
 #pragma unroll
-      for (int g = 0; g < EG; ++g) acc[g] = 0.0;
-      for (int kc0 = 0; kc0 < nkc; ++kc0) {
-        const int k0 = kc0 * EKC;
-        const int kc = d - k0 < EKC ? d - k0 : EKC;
-        __syncthreads();  // the previous chunk has been consumed
+      for (int rt = 0; rt < RT; ++rt) {
+        double v = __builtin_inf();
+        int jj = 0x7fffffff;
 #pragma unroll
-        for (int i = 0; i < EKC; ++i) {
-          const int e = tid + NT * i, rr = e / EKC, kk = e - rr * EKC;
-          xs[rr * EXS + kk] = v[i];
-        }
-        for (int e = tid; e < EKC * EG; e += NT) {
-          const int kk = e / EG, g = e - kk * EG;
-          cs[e] = (kk < kc && g < ng) ? cen[static_cast<size_t>(j0 + g) * d + k0 + kk] : 0.0;
-        }
-        __syncthreads();
-        const int c = pass * nkc + kc0;
-        if (c + 1 < npass * nkc) load(c + 1);  // in flight under this chunk's FMAs
-        for (int kk = 0; kk < kc; ++kk) {
-          const double xk = xs[tid * EXS + kk];
+        for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-          for (int g = 0; g < EG; ++g)
-            if (g < ng) acc[g] = __fma_rn(xk, cs[kk * EG + g], acc[g]);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < EG; ++g) {
-        if (g >= ng) break;
-        const int j = j0 + g;
-        const double dj = __fma_rn(-2.0, acc[g], cn[j]);
-        if (j == 0 || dj < best) {
-          best = dj;
-          lab = j;
+          for (int i = 0; i < 4; ++i) {
+            const int j = j0 + 16 * ct + q + 4 * i;
+            if (j < K) lexmin(v, jj, __fma_rn(-2.0, acc[rt][ct][i], cn[j]), j);
+          }
+        lexmin(v, jj, __shfl_xor(v, 16), __shfl_xor(jj, 16));
+        lexmin(v, jj, __shfl_xor(v, 32), __shfl_xor(jj, 32));
+        if (j0 == 0) {
+          bv[rt] = v;
+          bj[rt] = jj;
+        } else {
+          lexmin(bv[rt], bj[rt], v, jj);
         }
       }
     }
-    if (tid < nrows) w.lab[r0 + tid] = lab;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int r = (t0 + rt) * 16 + c16;
+      if (q == 0 && r < m) w.lab[r] = bj[rt];
+    }
+  }
+}
+
+__device__ __forceinline__ void estep_mfma(const WG& w, const double* cen, const double* cn, int K, int d, int m, int tid) {
+  if (K <= 16) estep_tiles<2, 1>(w, cen, cn, K, d, m, tid);
+  else estep_tiles<2, 2>(w, cen, cn, K, d, m, tid);
+  __syncthreads();
+}
+
+// k-means++ distances to the candidate rows cand[0 .. ntr) (ntr <= 6, the first centre: ntr = 1):
+// ((-2 x.c) + |c|^2) + |x|^2 clipped at 0, then min with the closest distance so far (dc[t][r]),
+// or, for the first centre, the closest distances themselves (cl[r]).
+__device__ __forceinline__ void kpp_mfma(const WG& w, int d, int m, const int* cand, int ntr, bool first, int tid) {
+  constexpr int RT = 2;
+  const int l = tid & 63, q = l >> 4, c16 = l & 15;
+  const int ntile = (m + 15) >> 4;
+  const double* pa[1] = {w.xc + static_cast<size_t>(cand[c16 < ntr ? c16 : ntr - 1]) * d + q};
+  for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
+    const double* pb[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int r = (t0 + rt) * 16 + c16;
+      pb[rt] = w.xc + static_cast<size_t>(r < m ? r : m - 1) * d + q;
+    }
+    f64x4 acc[RT][1];
+    mfma_dots<RT, 1>(pa, pb, d, q, acc);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int r = (t0 + rt) * 16 + c16;
+      if (r >= m) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // candidate t = q + 4i (< ntr <= 6)
+        const int t = q + 4 * i;
+        if (t >= ntr) continue;
+        double dd = -2.0 * acc[rt][0][i];
+        dd += w.xsq[cand[t]];
+        dd += w.xsq[r];
+        dd = dd > 0.0 ? dd : 0.0;
+        if (first) w.cl[r] = dd;
+        else w.dc[static_cast<size_t>(t) * m + r] = w.cl[r] < dd ? w.cl[r] : dd;
+      }
+    }
   }
   __syncthreads();
 }
@@ -292,14 +406,13 @@ __device__ __forceinline__ double xc(const F64Args& a, const int32_t* idx, const
   return a.X[static_cast<size_t>(idx[r]) * a.d + k] - mean[k];
 }
 
-__global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restrict__ pa) {
+__global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __restrict__ pa) {
   // arguments read from the workspace header (as in kmeans.hip): re-loaded where used rather
   // than pinned in SGPRs for the whole kernel
   const F64Args& a = *pa;
   __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[TMAX], s_map[KMAX + 1];
   __shared__ double s_pot[TMAX], s_tol, s_red[NT];
   __shared__ int s_ired[NT];
-  __shared__ double s_xs[NT * EXS], s_cs[EKC * EG];  // estep_block staging
   const int tid = threadIdx.x;
   char* base = a.ws + static_cast<size_t>(blockIdx.x) * a.per_wg;
   WG w;
@@ -317,12 +430,16 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
   w.ord = reinterpret_cast<int32_t*>(base + a.o_ord);
   __shared__ int s_off[KMAX + 2];
   const int m = a.m, d = a.d;
+#ifdef CC_F64_STAMPS
+  unsigned long long st_acc[10] = {}, st_t = wall_clock64();
+#endif
   for (;;) {
     __syncthreads();
     if (tid == 0) s_unit = static_cast<int>(atomicAdd(a.counter, 1u));
     __syncthreads();
     const int unit = s_unit;
     if (unit >= a.nh * a.nK) break;
+    F64_STAMP(7);
     const int hb = unit / a.nK, kk = unit - hb * a.nK;
     const int h = a.h_begin + hb;
     const int K = a.Ks[kk];
@@ -331,11 +448,27 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
 
     // column means (rows in order), then variances of the centred columns
     for (int k = tid; k < d; k += NT) {
+      // sums in row order, the loads of 8 rows in flight ahead of the adds
       double s = 0.0;
-      for (int r = 0; r < m; ++r) s += a.X[static_cast<size_t>(idx[r]) * d + k];
+      int r = 0;
+      for (; r + 8 <= m; r += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = a.X[static_cast<size_t>(idx[r + u]) * d + k];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+      }
+      for (; r < m; ++r) s += a.X[static_cast<size_t>(idx[r]) * d + k];
       const double mu = s / m;
       double q = 0.0;
-      for (int r = 0; r < m; ++r) {
+      for (r = 0; r + 8 <= m; r += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = a.X[static_cast<size_t>(idx[r + u]) * d + k] - mu;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q += v[u] * v[u];
+      }
+      for (; r < m; ++r) {
         const double t = a.X[static_cast<size_t>(idx[r]) * d + k] - mu;
         q += t * t;
       }
@@ -356,6 +489,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
       w.xsq[r] = einsum_sq([&](int k) { return x[k]; }, d);
     }
     __syncthreads();
+    F64_STAMP(0);
     const double tol = s_tol;
 
     double best_inertia = 0.0;
@@ -365,17 +499,9 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
       // ---- k-means++ -------------------------------------------------------------
       int cpos = a.kpp_pos[kk * a.n_init + init];
       for (int k = tid; k < d; k += NT) w.cen[k] = xrow(w, d, cpos)[k];
-      for (int r = tid; r < m; r += NT) {
-        const double* xq = xrow(w, d, cpos);
-        const double* xr = xrow(w, d, r);
-        double s0 = 0.0;
-        for (int k = 0; k < d; ++k) s0 = __fma_rn(xq[k], xr[k], s0);
-        double dd = -2.0 * s0;
-        dd += w.xsq[cpos];
-        dd += w.xsq[r];
-        w.cl[r] = dd > 0.0 ? dd : 0.0;
-      }
+      if (tid == 0) s_cand[0] = cpos;
       __syncthreads();
+      kpp_mfma(w, d, m, s_cand, 1, true, tid);
       if (tid == 0) s_pot[0] = blas_ddot_ones(w.cl, m);
       __syncthreads();
       double pot = s_pot[0];
@@ -385,44 +511,23 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
           const double rv = u[(c - 1) * ntr + tid] * pot;
           double cum = 0.0;
           int pos = m;
-          for (int r = 0; r < m; ++r) {
-            cum += w.cl[r];
-            if (!(cum < rv)) {
-              pos = r;
-              break;
-            }
+          // the running sum in row order, its loads 16 rows ahead of the adds (the walk was one
+          // dependent global load per row)
+          for (int r0 = 0; r0 < m && pos == m; r0 += 16) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = r0 + q < m ? w.cl[r0 + q] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+              if (pos == m && r0 + q < m) {
+                cum += v[q];
+                if (!(cum < rv)) pos = r0 + q;
+              }
           }
           s_cand[tid] = pos < m - 1 ? pos : m - 1;
         }
         __syncthreads();
-        for (int r = tid; r < m; r += NT) {
-          // the ntr candidates' dot products as independent sequential FMA chains
-          const double* xr = xrow(w, d, r);
-          const double* xq[TMAX];
-          double acc[TMAX];
-#pragma unroll
-          for (int t = 0; t < TMAX; ++t) {
-            xq[t] = xrow(w, d, s_cand[t < ntr ? t : 0]);
-            acc[t] = 0.0;
-          }
-          for (int k = 0; k < d; ++k) {
-            const double xk = xr[k];
-#pragma unroll
-            for (int t = 0; t < TMAX; ++t)
-              if (t < ntr) acc[t] = __fma_rn(xq[t][k], xk, acc[t]);
-          }
-#pragma unroll
-          for (int t = 0; t < TMAX; ++t) {
-            if (t >= ntr) break;
-            const int q = s_cand[t];
-            double dd = -2.0 * acc[t];
-            dd += w.xsq[q];
-            dd += w.xsq[r];
-            dd = dd > 0.0 ? dd : 0.0;
-            w.dc[static_cast<size_t>(t) * m + r] = w.cl[r] < dd ? w.cl[r] : dd;
-          }
-        }
-        __syncthreads();
+        kpp_mfma(w, d, m, s_cand, ntr, false, tid);
         if (tid < ntr) s_pot[tid] = blas_gemv_t_ones(w.dc + static_cast<size_t>(tid) * m, m, tid, ntr);
         __syncthreads();
         int bt = 0;
@@ -434,6 +539,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
         for (int k = tid; k < d; k += NT) w.cen[static_cast<size_t>(c) * d + k] = xrow(w, d, cpos)[k];
         __syncthreads();
       }
+      F64_STAMP(1);
       // ---- Lloyd -------------------------------------------------------------------
       for (int r = tid; r < m; r += NT) w.lold[r] = -1;
       bool strict = false;
@@ -451,9 +557,13 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
         int chg = 0;
         for (int j = tid; j < K; j += NT) s_ired[j] = 0;
         __syncthreads();
-        estep_block(w, cen, s_red, K, d, m, s_xs, s_cs, tid);
+        estep_mfma(w, cen, s_red, K, d, m, tid);
+        F64_STAMP(2);
+#ifdef CC_F64_STAMPS
+        if (tid == 0) st_acc[8] += 1;
+#endif
         for (int r = tid; r < m; r += NT) {
-          const int lab = w.lab[r];  // written by this thread in estep_block
+          const int lab = w.lab[r];
           chg |= (lab != w.lold[r]);
           atomicAdd(&s_ired[lab], 1);  // counts (integers: order-free)
         }
@@ -485,6 +595,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
           }
         }
         __syncthreads();
+        F64_STAMP(3);
         for (int p = tid; p < K * d; p += NT) {
           const int j = p / d, k = p - (p / d) * d;
           const int i0 = s_off[j], i1 = s_off[j + 1];
@@ -501,6 +612,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
           cnew[static_cast<size_t>(j) * d + k] = sum;
         }
         __syncthreads();
+        F64_STAMP(4);
         if (tid == 0) {
           int ne = 0;
           for (int j = 0; j < K; ++j) ne += (s_ired[j] == 0);
@@ -602,6 +714,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
           s_red[tid] = sh * sh;  // (the |c|^2 of this iteration are no longer read)
         }
         __syncthreads();
+        F64_STAMP(5);
         double* tmp = cen;
         cen = cnew;
         cnew = tmp;
@@ -621,7 +734,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
           s_red[j] = einsum_sq([&](int k) { return cj[k]; }, d);
         }
         __syncthreads();
-        estep_block(w, cen, s_red, K, d, m, s_xs, s_cs, tid);
+        estep_mfma(w, cen, s_red, K, d, m, tid);
       }
       // inertia: per-row squared distance to its centre, summed in row order
       for (int r = tid; r < m; r += NT) {
@@ -673,6 +786,7 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
         best_iter = n_iter;
       }
       __syncthreads();
+      F64_STAMP(6);
     }
     uint8_t* out = a.labels + static_cast<size_t>(kk) * a.n * a.ldl + h;
     for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = w.lbest[r];
@@ -681,6 +795,12 @@ __global__ __launch_bounds__(NT) void kmeans_f64_kernel(const F64Args* __restric
       if (a.niter_out) a.niter_out[static_cast<size_t>(kk) * a.H + h] = best_iter;
     }
   }
+#ifdef CC_F64_STAMPS
+  if (tid == 0) {
+    st_acc[9] = 1;
+    for (int q = 0; q < 10; ++q) atomicAdd(&cc_f64_stamps[q], st_acc[q]);
+  }
+#endif
 }
 
 struct F64Layout {
@@ -711,6 +831,15 @@ constexpr size_t WS_ARGS = 64;  // the work counter at 0, the kernel's F64Args a
 constexpr size_t WS_HEADER = (WS_ARGS + sizeof(F64Args) + 255) / 256 * 256;
 
 }  // namespace
+
+#ifdef CC_F64_STAMPS
+// the accumulated stamps (then zeroed): [0..7] phase clocks, [8] Lloyd iterations, [9] workgroups
+extern "C" int cc_kmeans_f64_stamps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cc_f64_stamps), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  const unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(cc_f64_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks, int nK, int grid) {
   if (m <= 0 || d <= 0 || !Ks || nK <= 0 || grid <= 0) return 0;
