@@ -401,6 +401,152 @@ __device__ __forceinline__ void kpp_mfma(const WG& w, int d, int m, const int* c
   __syncthreads();
 }
 
+// ---- k-means++ reductions over the closest distances ---------------------------------------------
+// The candidate search and the potentials are sequential reductions over m values; each was one
+// thread walking global memory (a load latency per few rows).  Now the same additions, in the
+// same order, run over LDS-staged blocks (the search) or as independent chains spread over the
+// workgroup (the BLAS potentials, whose accumulators are independent until their final folds).
+constexpr int CB = 1024;  // search staging block (doubles); the LDS area holds 2 * CB
+
+// cand[t] = searchsorted(cumsum(cl), u[t] * pot) clipped to m - 1, t < ntr.  Thread 0 runs the
+// float64 cumulative sum in row order over LDS blocks (the workgroup stages the next block
+// meanwhile); the running sum is non-decreasing, so the thresholds, sorted, are crossed in order.
+__device__ void kpp_search(const WG& w, int m, const double* u, double pot, int ntr, int* cand,
+                           double* sb, int* sflag, double* s_thr, int* s_tix, int tid) {
+  if (tid == 0) {
+    for (int t = 0; t < ntr; ++t) {
+      s_thr[t] = u[t] * pot;
+      s_tix[t] = t;
+    }
+    for (int t = 1; t < ntr; ++t)  // insertion sort of the thresholds (ties: either order)
+      for (int v = t; v > 0 && s_thr[v] < s_thr[v - 1]; --v) {
+        const double x = s_thr[v];
+        s_thr[v] = s_thr[v - 1];
+        s_thr[v - 1] = x;
+        const int y = s_tix[v];
+        s_tix[v] = s_tix[v - 1];
+        s_tix[v - 1] = y;
+      }
+    for (int t = 0; t < ntr; ++t) cand[t] = m - 1;  // not crossed: clipped to m - 1
+    *sflag = 0;
+  }
+  for (int e = tid; e < CB && e < m; e += NT) sb[e] = w.cl[e];
+  __syncthreads();
+  double cum = 0.0, tn = s_thr[0];
+  int next = 0;
+  int buf = 0;
+  for (int b0 = 0; b0 < m; b0 += CB) {
+    const int nb = b0 + CB;
+    double* nxt = sb + (buf ^ 1) * CB;
+    for (int e = tid; e < CB && nb + e < m; e += NT) nxt[e] = w.cl[nb + e];
+    if (tid == 0) {
+      const double* cur = sb + buf * CB;
+      const int n = m - b0 < CB ? m - b0 : CB;
+      for (int i0 = 0; i0 < n && next < ntr; i0 += 8) {
+        // 8 partial sums, then one comparison with the next threshold (the sums do not decrease)
+        double cs[8];
+        const int g = n - i0 < 8 ? n - i0 : 8;
+        double c = cum;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (i < g) c += cur[i0 + i];
+          cs[i] = c;
+        }
+        if (!(c < tn)) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            while (i < g && next < ntr && !(cs[i] < tn)) {
+              const int p = b0 + i0 + i;
+              cand[s_tix[next]] = p < m - 1 ? p : m - 1;
+              ++next;
+              tn = next < ntr ? s_thr[next] : 0.0;
+            }
+        }
+        cum = c;
+      }
+      if (next >= ntr) *sflag = 1;
+    }
+    __syncthreads();
+    if (*sflag) break;
+    buf ^= 1;
+  }
+  __syncthreads();
+}
+
+// a chain x[i0], x[i0 + L], ... (i < e) summed left to right from 0.0, loads 16 ahead
+__device__ __forceinline__ double chain_sum(const double* x, int i0, int e, int L) {
+  double acc = 0.0;
+  for (int i = i0; i < e; i += 16 * L) {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = i + k * L < e ? x[i + k * L] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (i + k * L < e) acc += v[k];
+  }
+  return acc;
+}
+
+// s_pot[t] = blas_gemv_t_ones(dc + t m, m, t, ntr) for t < ntr, its (column, 2048-row block, lane)
+// accumulator chains one per thread (part: an LDS area of 2 * CB doubles), the folds by thread t
+__device__ void kpp_pots(const WG& w, int m, int ntr, double* part, double* pot, int tid) {
+  const int n4 = ntr & ~3, rem = ntr - n4;
+  const int m1 = m & ~3;
+  const int nb = (m1 + 2047) / 2048;
+  const int G = (2 * CB) / (ntr * 4);  // blocks per round
+  double y = 0.0;
+  for (int bb = 0; bb < nb; bb += G) {
+    const int gb = nb - bb < G ? nb - bb : G;
+    for (int ch = tid; ch < ntr * gb * 4; ch += NT) {
+      const int t = ch / (gb * 4), g = (ch >> 2) % gb, q = ch & 3;
+      const int L = (rem >= 2 && t >= n4 && t < n4 + 2) ? 2 : 4;
+      if (q >= L) continue;
+      const int b = (bb + g) * 2048, e = b + 2048 < m1 ? b + 2048 : m1;
+      part[(t * G + g) * 4 + q] = chain_sum(w.dc + static_cast<size_t>(t) * m, b + q, e, L);
+    }
+    __syncthreads();
+    if (tid < ntr) {
+      const bool two = rem >= 2 && tid >= n4 && tid < n4 + 2;
+      for (int g = 0; g < gb; ++g) {
+        const double* pp = part + (tid * G + g) * 4;
+        y += two ? pp[0] + pp[1] : (pp[0] + pp[2]) + (pp[1] + pp[3]);
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < ntr) {
+    if (m1 < m) {
+      const double* x = w.dc + static_cast<size_t>(tid) * m;
+      double t = x[m1];
+      for (int i = m1 + 1; i < m; ++i) t += x[i];
+      y += t;
+    }
+    pot[tid] = y;
+  }
+  __syncthreads();
+}
+
+// *out = blas_ddot_ones(cl, m), its 32 accumulator chains one per thread, the folds by thread 0
+__device__ void kpp_pot0(const WG& w, int m, double* part, double* out, int tid) {
+  const int n1 = m & -16, n32 = n1 & ~31;
+  if (tid < 32) part[tid] = chain_sum(w.cl, tid, n32, 32);  // Z[a][q] = chain of x[i + 8a + q]
+  __syncthreads();
+  if (tid == 0) {
+    double A[4][4];
+    for (int a = 0; a < 4; ++a)
+      for (int q = 0; q < 4; ++q) A[a][q] = part[8 * a + q] + part[8 * a + q + 4];
+    for (int i = n32; i < n1; i += 16)
+      for (int a = 0; a < 4; ++a)
+        for (int q = 0; q < 4; ++q) A[a][q] += w.cl[i + 4 * a + q];
+    double L[4];
+    for (int q = 0; q < 4; ++q) L[q] = ((A[0][q] + A[1][q]) + A[2][q]) + A[3][q];
+    double dot = (L[0] + L[2]) + (L[1] + L[3]);
+    for (int i = n1; i < m; ++i) dot += w.cl[i];
+    *out = dot;
+  }
+  __syncthreads();
+}
+
 // centred feature k of resample row r
 __device__ __forceinline__ double xc(const F64Args& a, const int32_t* idx, const double* mean, int r, int k) {
   return a.X[static_cast<size_t>(idx[r]) * a.d + k] - mean[k];
@@ -413,6 +559,9 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[TMAX], s_map[KMAX + 1];
   __shared__ double s_pot[TMAX], s_tol, s_red[NT];
   __shared__ int s_ired[NT];
+  __shared__ double s_stage[2 * CB];  // k-means++ search blocks / potential partials
+  __shared__ double s_thr[TMAX];
+  __shared__ int s_tix[TMAX];
   const int tid = threadIdx.x;
   char* base = a.ws + static_cast<size_t>(blockIdx.x) * a.per_wg;
   WG w;
@@ -502,34 +651,13 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
       if (tid == 0) s_cand[0] = cpos;
       __syncthreads();
       kpp_mfma(w, d, m, s_cand, 1, true, tid);
-      if (tid == 0) s_pot[0] = blas_ddot_ones(w.cl, m);
-      __syncthreads();
+      kpp_pot0(w, m, s_stage, &s_pot[0], tid);
       double pot = s_pot[0];
       for (int c = 1; c < K; ++c) {
         // candidates: searchsorted(cumsum(closest), u * pot), clipped to m - 1
-        if (tid < ntr) {
-          const double rv = u[(c - 1) * ntr + tid] * pot;
-          double cum = 0.0;
-          int pos = m;
-          // the running sum in row order, its loads 16 rows ahead of the adds (the walk was one
-          // dependent global load per row)
-          for (int r0 = 0; r0 < m && pos == m; r0 += 16) {
-            double v[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = r0 + q < m ? w.cl[r0 + q] : 0.0;
-#pragma unroll
-            for (int q = 0; q < 16; ++q)
-              if (pos == m && r0 + q < m) {
-                cum += v[q];
-                if (!(cum < rv)) pos = r0 + q;
-              }
-          }
-          s_cand[tid] = pos < m - 1 ? pos : m - 1;
-        }
-        __syncthreads();
+        kpp_search(w, m, u + (c - 1) * ntr, pot, ntr, s_cand, s_stage, &s_flag, s_thr, s_tix, tid);
         kpp_mfma(w, d, m, s_cand, ntr, false, tid);
-        if (tid < ntr) s_pot[tid] = blas_gemv_t_ones(w.dc + static_cast<size_t>(tid) * m, m, tid, ntr);
-        __syncthreads();
+        kpp_pots(w, m, ntr, s_stage, s_pot, tid);
         int bt = 0;
         for (int t = 1; t < ntr; ++t)
           if (s_pot[t] < s_pot[bt]) bt = t;
