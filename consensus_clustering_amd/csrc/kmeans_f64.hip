@@ -72,7 +72,7 @@ struct F64Args {
   unsigned* counter;
   char* ws;
   size_t per_wg;
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_ord;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc;
 };
 
 // numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) of a contiguous double array:
@@ -223,7 +223,7 @@ __device__ unsigned long long cc_f64_stamps[16];
 
 struct WG {
   double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew, *xc;
-  int32_t *lab, *lold, *ord;
+  int32_t *lab, *lold;
   uint8_t* lbest;
 };
 
@@ -398,6 +398,76 @@ __device__ __forceinline__ void kpp_mfma(const WG& w, int d, int m, const int* c
       }
     }
   }
+  __syncthreads();
+}
+
+// The centre sums on the matrix cores: cnew[j][k] = sum over the rows r, in row order, of
+// [lab[r] == j] * x[r][k], one sequential FMA chain per output over k-steps of 4 rows (A = the
+// one-hot labels: lane l cluster l & 15, row 4s + (l >> 4); B = the rows: lane l feature l & 15).
+// fma(1, x, acc) = acc + x is sklearn's addition (centers_new[j] += x * 1.0); fma(0, x, acc) =
+// acc + (+-0) = acc exactly for finite x, the accumulators starting at +0 and never -0 - so each
+// output is the row-order sum of its cluster's rows, as the list walk computed it.  A wave owns
+// CTP cluster tiles x one 16-feature tile per pass over the rows; the passes cover the rows' 16-
+// feature slices once.
+template <int CTP>
+__device__ void msum_tiles(const WG& w, double* cnew, int K, int d, int m, int tid) {
+  const int l = tid & 63, q = l >> 4, c16 = l & 15;
+  const int nct = (K + 15) >> 4, nft = (d + 15) >> 4;
+  const int ncg = (nct + CTP - 1) / CTP;
+  const int S = (m + 3) >> 2;
+  for (int item = tid >> 6; item < ncg * nft; item += NT / 64) {
+    const int cg = item / nft, ft = item - cg * nft;
+    const int f = ft * 16 + c16;
+    const double* pb = w.xc + (f < d ? f : d - 1) + static_cast<size_t>(q) * d;
+    const int32_t* pl = w.lab + q;
+    int jl[CTP];
+    f64x4 acc[CTP];
+#pragma unroll
+    for (int ct = 0; ct < CTP; ++ct) {
+      jl[ct] = (cg * CTP + ct) * 16 + c16;
+      acc[ct] = f64x4{0.0, 0.0, 0.0, 0.0};
+    }
+    int lb0[MG], lb1[MG];
+    double b0[MG], b1[MG];
+    auto ld = [&](int (&lv)[MG], double (&bv)[MG], int s0) __attribute__((always_inline)) {
+      if (s0 >= S) return;
+#pragma unroll
+      for (int i = 0; i < MG; ++i) {
+        const int r = 4 * (s0 + i) + q;
+        const bool in = s0 + i < S && r < m;
+        lv[i] = in ? pl[4 * (s0 + i)] : -1;
+        bv[i] = in ? pb[static_cast<size_t>(4 * (s0 + i)) * d] : 0.0;
+      }
+    };
+    auto mm = [&](const int (&lv)[MG], const double (&bv)[MG], int s0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < MG; ++i)
+        if (s0 + i < S)
+#pragma unroll
+          for (int ct = 0; ct < CTP; ++ct)
+            acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(lv[i] == jl[ct] ? 1.0 : 0.0, bv[i], acc[ct], 0, 0, 0);
+    };
+    ld(lb0, b0, 0);
+    for (int s0 = 0; s0 < S; s0 += 2 * MG) {
+      ld(lb1, b1, s0 + MG);
+      mm(lb0, b0, s0);
+      ld(lb0, b0, s0 + 2 * MG);
+      mm(lb1, b1, s0 + MG);
+    }
+    if (f < d)
+#pragma unroll
+      for (int ct = 0; ct < CTP; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = (cg * CTP + ct) * 16 + q + 4 * i;
+          if (j < K) cnew[static_cast<size_t>(j) * d + f] = acc[ct][i];
+        }
+  }
+}
+
+__device__ __forceinline__ void msum_mfma(const WG& w, double* cnew, int K, int d, int m, int tid) {
+  if (K <= 16) msum_tiles<1>(w, cnew, K, d, m, tid);
+  else msum_tiles<2>(w, cnew, K, d, m, tid);
   __syncthreads();
 }
 
@@ -576,8 +646,6 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   w.lold = reinterpret_cast<int32_t*>(base + a.o_lold);
   w.lbest = reinterpret_cast<uint8_t*>(base + a.o_lbest);
   w.xc = reinterpret_cast<double*>(base + a.o_xc);
-  w.ord = reinterpret_cast<int32_t*>(base + a.o_ord);
-  __shared__ int s_off[KMAX + 2];
   const int m = a.m, d = a.d;
 #ifdef CC_F64_STAMPS
   unsigned long long st_acc[10] = {}, st_t = wall_clock64();
@@ -696,50 +764,8 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
           atomicAdd(&s_ired[lab], 1);  // counts (integers: order-free)
         }
         const int changed = __syncthreads_or(chg);
-        // centre sums in row order: the rows of each cluster listed in row order (offsets by
-        // cluster, then one wave per cluster compacting 64 rows per ballot), then one thread per
-        // (cluster, feature) summing its list sequentially: the same additions, in the same order,
-        // as sklearn's row loop
-        if (tid == 0) {
-          int o = 0;
-          for (int j = 0; j < K; ++j) {
-            s_off[j] = o;
-            o += s_ired[j];
-          }
-          s_off[K] = o;
-        }
-        __syncthreads();
-        {
-          const int wv = tid >> 6, ln = tid & 63;
-          for (int j = wv; j < K; j += NT / 64) {
-            int pos = s_off[j];
-            for (int b = 0; b < m; b += 64) {
-              const int r = b + ln;
-              const bool hit = r < m && w.lab[r] == j;
-              const unsigned long long msk = __ballot(hit);
-              if (hit) w.ord[pos + __popcll(msk & ((1ull << ln) - 1ull))] = r;
-              pos += __popcll(msk);
-            }
-          }
-        }
-        __syncthreads();
         F64_STAMP(3);
-        for (int p = tid; p < K * d; p += NT) {
-          const int j = p / d, k = p - (p / d) * d;
-          const int i0 = s_off[j], i1 = s_off[j + 1];
-          double sum = 0.0;
-          int i = i0;
-          for (; i + 8 <= i1; i += 8) {  // the loads of 8 rows in flight, added in order
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = xrow(w, d, w.ord[i + u])[k];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) sum += v[u];
-          }
-          for (; i < i1; ++i) sum += xrow(w, d, w.ord[i])[k];
-          cnew[static_cast<size_t>(j) * d + k] = sum;
-        }
-        __syncthreads();
+        msum_mfma(w, cnew, K, d, m, tid);
         F64_STAMP(4);
         if (tid == 0) {
           int ne = 0;
@@ -932,7 +958,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
 }
 
 struct F64Layout {
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_ord, per_wg;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, per_wg;
 };
 
 F64Layout f64_layout(int m, int d, int kmax) {
@@ -950,7 +976,6 @@ F64Layout f64_layout(int m, int d, int kmax) {
   L.o_lold = o;  o += al(sizeof(int32_t) * m);
   L.o_lbest = o; o += al(m);
   L.o_xc = o;    o += al(sizeof(double) * static_cast<size_t>(m) * d);
-  L.o_ord = o;   o += al(sizeof(int32_t) * m);
   L.per_wg = o;
   return L;
 }
@@ -1044,7 +1069,6 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.o_lold = L.o_lold;
   a.o_lbest = L.o_lbest;
   a.o_xc = L.o_xc;
-  a.o_ord = L.o_ord;
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nK));
   // one upload: the zeroed counter and the arguments (a pageable source is consumed before
   // hipMemcpyAsync returns)
