@@ -213,8 +213,8 @@ __device__ unsigned long long cc_f64_stamps[16];
   do {                                              \
     if (tid == 0) {                                 \
       const unsigned long long t_ = wall_clock64(); \
-      st_acc[ph] += t_ - st_t;                      \
-      st_t = t_;                                    \
+      st_acc[ph] += t_ - st_acc[10];                \
+      st_acc[10] = t_;                              \
     }                                               \
   } while (0)
 #else
@@ -648,7 +648,12 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   w.xc = reinterpret_cast<double*>(base + a.o_xc);
   const int m = a.m, d = a.d;
 #ifdef CC_F64_STAMPS
-  unsigned long long st_acc[10] = {}, st_t = wall_clock64();
+  // the accumulators in LDS (thread 0's registers would move the kernel's allocation)
+  __shared__ unsigned long long st_acc[11];
+  if (tid == 0) {
+    for (int q = 0; q < 10; ++q) st_acc[q] = 0;
+    st_acc[10] = wall_clock64();
+  }
 #endif
   for (;;) {
     __syncthreads();
