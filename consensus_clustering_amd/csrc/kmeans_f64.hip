@@ -407,45 +407,59 @@ __device__ __forceinline__ void kpp_mfma(const WG& w, int d, int m, const int* c
 // fma(1, x, acc) = acc + x is sklearn's addition (centers_new[j] += x * 1.0); fma(0, x, acc) =
 // acc + (+-0) = acc exactly for finite x, the accumulators starting at +0 and never -0 - so each
 // output is the row-order sum of its cluster's rows, as the list walk computed it.  A wave owns
-// CTP cluster tiles x one 16-feature tile per pass over the rows; the passes cover the rows' 16-
+// CTP cluster tiles x FTP 16-feature tiles per pass over the rows; the passes cover the rows'
 // feature slices once.
-template <int CTP>
+// FTP feature tiles per pass: FTP independent chains per cluster tile (the issue of one chain's
+// dependent MFMAs alone leaves the matrix core idle).
+template <int CTP, int FTP>
 __device__ void msum_tiles(const WG& w, double* cnew, int K, int d, int m, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int nct = (K + 15) >> 4, nft = (d + 15) >> 4;
+  const int nfg = (nft + FTP - 1) / FTP;
   const int ncg = (nct + CTP - 1) / CTP;
   const int S = (m + 3) >> 2;
-  for (int item = tid >> 6; item < ncg * nft; item += NT / 64) {
-    const int cg = item / nft, ft = item - cg * nft;
-    const int f = ft * 16 + c16;
-    const double* pb = w.xc + (f < d ? f : d - 1) + static_cast<size_t>(q) * d;
+  for (int item = tid >> 6; item < ncg * nfg; item += NT / 64) {
+    const int cg = item / nfg, fg = item - cg * nfg;
+    int f[FTP];
+    const double* pb[FTP];
+#pragma unroll
+    for (int u = 0; u < FTP; ++u) {
+      f[u] = (fg * FTP + u) * 16 + c16;
+      pb[u] = w.xc + (f[u] < d ? f[u] : d - 1) + static_cast<size_t>(q) * d;
+    }
     const int32_t* pl = w.lab + q;
     int jl[CTP];
-    f64x4 acc[CTP];
+    f64x4 acc[CTP][FTP];
 #pragma unroll
     for (int ct = 0; ct < CTP; ++ct) {
       jl[ct] = (cg * CTP + ct) * 16 + c16;
-      acc[ct] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int u = 0; u < FTP; ++u) acc[ct][u] = f64x4{0.0, 0.0, 0.0, 0.0};
     }
     int lb0[MG], lb1[MG];
-    double b0[MG], b1[MG];
-    auto ld = [&](int (&lv)[MG], double (&bv)[MG], int s0) __attribute__((always_inline)) {
+    double b0[MG][FTP], b1[MG][FTP];
+    auto ld = [&](int (&lv)[MG], double (&bv)[MG][FTP], int s0) __attribute__((always_inline)) {
       if (s0 >= S) return;
 #pragma unroll
       for (int i = 0; i < MG; ++i) {
         const int r = 4 * (s0 + i) + q;
         const bool in = s0 + i < S && r < m;
         lv[i] = in ? pl[4 * (s0 + i)] : -1;
-        bv[i] = in ? pb[static_cast<size_t>(4 * (s0 + i)) * d] : 0.0;
+#pragma unroll
+        for (int u = 0; u < FTP; ++u) bv[i][u] = in ? pb[u][static_cast<size_t>(4 * (s0 + i)) * d] : 0.0;
       }
     };
-    auto mm = [&](const int (&lv)[MG], const double (&bv)[MG], int s0) __attribute__((always_inline)) {
+    auto mm = [&](const int (&lv)[MG], const double (&bv)[MG][FTP], int s0) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MG; ++i)
         if (s0 + i < S)
 #pragma unroll
-          for (int ct = 0; ct < CTP; ++ct)
-            acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(lv[i] == jl[ct] ? 1.0 : 0.0, bv[i], acc[ct], 0, 0, 0);
+          for (int ct = 0; ct < CTP; ++ct) {
+            const double av = lv[i] == jl[ct] ? 1.0 : 0.0;
+#pragma unroll
+            for (int u = 0; u < FTP; ++u)
+              acc[ct][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[i][u], acc[ct][u], 0, 0, 0);
+          }
     };
     ld(lb0, b0, 0);
     for (int s0 = 0; s0 < S; s0 += 2 * MG) {
@@ -454,20 +468,29 @@ __device__ void msum_tiles(const WG& w, double* cnew, int K, int d, int m, int t
       ld(lb0, b0, s0 + 2 * MG);
       mm(lb1, b1, s0 + MG);
     }
-    if (f < d)
 #pragma unroll
-      for (int ct = 0; ct < CTP; ++ct)
+    for (int u = 0; u < FTP; ++u)
+      if (f[u] < d)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int j = (cg * CTP + ct) * 16 + q + 4 * i;
-          if (j < K) cnew[static_cast<size_t>(j) * d + f] = acc[ct][i];
-        }
+        for (int ct = 0; ct < CTP; ++ct)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int j = (cg * CTP + ct) * 16 + q + 4 * i;
+            if (j < K) cnew[static_cast<size_t>(j) * d + f[u]] = acc[ct][u][i];
+          }
   }
 }
 
+// two feature tiles (two more independent chains) per wave where every wave still gets a pass
 __device__ __forceinline__ void msum_mfma(const WG& w, double* cnew, int K, int d, int m, int tid) {
-  if (K <= 16) msum_tiles<1>(w, cnew, K, d, m, tid);
-  else msum_tiles<2>(w, cnew, K, d, m, tid);
+  const bool two = ((d + 31) >> 5) * (K <= 16 ? 1 : (((K + 15) >> 4) + 1) / 2) >= NT / 64;
+  if (K <= 16) {
+    if (two) msum_tiles<1, 2>(w, cnew, K, d, m, tid);
+    else msum_tiles<1, 1>(w, cnew, K, d, m, tid);
+  } else {
+    if (two) msum_tiles<2, 2>(w, cnew, K, d, m, tid);
+    else msum_tiles<2, 1>(w, cnew, K, d, m, tid);
+  }
   __syncthreads();
 }
 
