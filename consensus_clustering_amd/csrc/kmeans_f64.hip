@@ -33,7 +33,8 @@
 // the results are bit-identical to the previous kernel (and to sklearn where it was).
 // The E-step and the k-means++ distances run on the float64 matrix cores (v_mfma_f64_16x16x4_f64,
 // whose per-output accumulation is the sequential FMA chain: see mfma_dots), 16 rows x 16 centres
-// per instruction, the operands read straight from the row-major centred rows.
+// per instruction; the rows enter as B operands from a fragment-ordered copy of the centred rows
+// (one contiguous 512-B load per k-step and row tile), the centres straight from their rows.
 #include <hip/hip_runtime.h>
 #include <cstring>
 
@@ -72,7 +73,7 @@ struct F64Args {
   unsigned* counter;
   char* ws;
   size_t per_wg;
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf;
 };
 
 // numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) of a contiguous double array:
@@ -222,7 +223,7 @@ __device__ unsigned long long cc_f64_stamps[16];
 #endif
 
 struct WG {
-  double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew, *xc;
+  double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew, *xc, *xf;
   int32_t *lab, *lold;
   uint8_t* lbest;
 };
@@ -237,15 +238,18 @@ __device__ __forceinline__ const double* xrow(const WG& w, int d, int r) { retur
 // fma(a3, b3, fma(a2, b2, fma(a1, b1, fma(a0, b0, c)))) on 2^20 mixed-exponent results
 // (tools/mfma_f64_probe.hip, profiles/r04/mfma_f64_probe.txt).  A chain of them over k-steps
 // 0 .. d/4-1 is therefore the same sequential FMA dot product (the small-matrix dgemm order) the
-// VALU loops computed, 1024 FMAs per instruction, its operands read straight from the row-major
-// rows (lane l: row l & 15, feature 4s + (l >> 4); consecutive steps reuse the same cache lines).
+// VALU loops computed, 1024 FMAs per instruction (lane l: row l & 15, feature 4s + (l >> 4)).
+// The A operands (centres, candidates) are read from their row-major rows (consecutive steps reuse
+// the same cache lines); the B operands (the unit's rows) from the fragment image o_xf, built once
+// per unit, at step stride BS = 64: 16 scattered 32-B pieces per load became one 512-B piece
+// (E-step 1.3-1.6x per iteration, profiles/r04/f64_budget_r4ak.txt).
 // Orientation: A = 16 "centres", B = 16 rows; D's lane l holds row l & 15 against centres
 // (l >> 4) + 4i, i = 0..3.  Features past d (d % 4 != 0) enter as exact zeros in both operands:
 // fma(0, 0, acc) = acc for the accumulators here (never -0: they start at +0).
 using f64x4 = __attribute__((ext_vector_type(4))) double;
 constexpr int MG = 4;  // k-steps per operand load group; two groups in flight
 
-template <int RT, int CT>
+template <int RT, int CT, int BS = 4>
 __device__ __forceinline__ void mfma_dots(const double* const (&pa)[CT], const double* const (&pb)[RT], int d,
                                           int q, f64x4 (&acc)[RT][CT]) {
 #pragma unroll
@@ -262,7 +266,7 @@ __device__ __forceinline__ void mfma_dots(const double* const (&pa)[CT], const d
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) a[i][ct] = pa[ct][4 * s];
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) b[i][rt] = pb[rt][4 * s];
+      for (int rt = 0; rt < RT; ++rt) b[i][rt] = pb[rt][BS * s];
     }
   };
   auto mm = [&](const double (&a)[MG][CT], const double (&b)[MG][RT], int s0) __attribute__((always_inline)) {
@@ -286,7 +290,7 @@ __device__ __forceinline__ void mfma_dots(const double* const (&pa)[CT], const d
     const bool in = 4 * S + q < d;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      const double bv = in ? pb[rt][4 * S] : 0.0;
+      const double bv = in ? pb[rt][BS * S] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
         acc[rt][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? pa[ct][4 * S] : 0.0, bv, acc[rt][ct], 0, 0, 0);
@@ -314,10 +318,8 @@ __device__ void estep_tiles(const WG& w, const double* cen, const double* cn, in
   for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
     const double* pb[RT];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int r = (t0 + rt) * 16 + c16;
-      pb[rt] = w.xc + static_cast<size_t>(r < m ? r : m - 1) * d + q;
-    }
+    for (int rt = 0; rt < RT; ++rt)  // the row tiles in the fragment image (past the last: clamped)
+      pb[rt] = w.xf + static_cast<size_t>(t0 + rt < ntile ? t0 + rt : ntile - 1) * ((d + 3) >> 2) * 64 + l;
     double bv[RT];
     int bj[RT];
     for (int j0 = 0; j0 < K; j0 += 16 * CT) {
@@ -328,7 +330,7 @@ __device__ void estep_tiles(const WG& w, const double* cen, const double* cn, in
         pa[ct] = cen + static_cast<size_t>(j < K ? j : K - 1) * d + q;
       }
       f64x4 acc[RT][CT];
-      mfma_dots<RT, CT>(pa, pb, d, q, acc);
+      mfma_dots<RT, CT, 64>(pa, pb, d, q, acc);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         double v = __builtin_inf();
@@ -375,12 +377,10 @@ __device__ __forceinline__ void kpp_mfma(const WG& w, int d, int m, const int* c
   for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
     const double* pb[RT];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int r = (t0 + rt) * 16 + c16;
-      pb[rt] = w.xc + static_cast<size_t>(r < m ? r : m - 1) * d + q;
-    }
+    for (int rt = 0; rt < RT; ++rt)
+      pb[rt] = w.xf + static_cast<size_t>(t0 + rt < ntile ? t0 + rt : ntile - 1) * ((d + 3) >> 2) * 64 + l;
     f64x4 acc[RT][1];
-    mfma_dots<RT, 1>(pa, pb, d, q, acc);
+    mfma_dots<RT, 1, 64>(pa, pb, d, q, acc);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int r = (t0 + rt) * 16 + c16;
@@ -669,6 +669,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   w.lold = reinterpret_cast<int32_t*>(base + a.o_lold);
   w.lbest = reinterpret_cast<uint8_t*>(base + a.o_lbest);
   w.xc = reinterpret_cast<double*>(base + a.o_xc);
+  w.xf = reinterpret_cast<double*>(base + a.o_xf);
   const int m = a.m, d = a.d;
 #ifdef CC_F64_STAMPS
   // the accumulators in LDS (thread 0's registers would move the kernel's allocation)
@@ -726,6 +727,21 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
     for (size_t e = tid; e < static_cast<size_t>(m) * d; e += NT) {
       const int r = static_cast<int>(e / d), k = static_cast<int>(e - static_cast<size_t>(r) * d);
       w.xc[e] = xc(a, idx, w.mean, r, k);
+    }
+    __syncthreads();
+    // the same values as the matrix cores' B operand image: row tile t, k-step s, lane l holds
+    // row 16t + (l & 15), feature 4s + (l >> 4) (exact zeros past m and d), so every operand
+    // load of a k-step is one contiguous 512-B piece
+    {
+      const int S4 = (d + 3) >> 2;
+      const size_t nf = static_cast<size_t>((m + 15) >> 4) * S4 * 64;
+      for (size_t e = tid; e < nf; e += NT) {
+        const int l = static_cast<int>(e & 63);
+        const size_t ts = e >> 6;
+        const int t = static_cast<int>(ts / S4), sk = static_cast<int>(ts - static_cast<size_t>(t) * S4);
+        const int r = 16 * t + (l & 15), k = 4 * sk + (l >> 4);
+        w.xf[e] = (r < m && k < d) ? w.xc[static_cast<size_t>(r) * d + k] : 0.0;
+      }
     }
     __syncthreads();
     // squared row norms of the centred rows
@@ -986,7 +1002,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
 }
 
 struct F64Layout {
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, per_wg;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf, per_wg;
 };
 
 F64Layout f64_layout(int m, int d, int kmax) {
@@ -1004,6 +1020,7 @@ F64Layout f64_layout(int m, int d, int kmax) {
   L.o_lold = o;  o += al(sizeof(int32_t) * m);
   L.o_lbest = o; o += al(m);
   L.o_xc = o;    o += al(sizeof(double) * static_cast<size_t>(m) * d);
+  L.o_xf = o;    o += al(sizeof(double) * static_cast<size_t>((m + 15) / 16) * 16 * ((d + 3) / 4) * 4);
   L.per_wg = o;
   return L;
 }
@@ -1097,6 +1114,7 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.o_lold = L.o_lold;
   a.o_lbest = L.o_lbest;
   a.o_xc = L.o_xc;
+  a.o_xf = L.o_xf;
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nK));
   // one upload: the zeroed counter and the arguments (a pageable source is consumed before
   // hipMemcpyAsync returns)

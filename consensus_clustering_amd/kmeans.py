@@ -228,7 +228,11 @@ class BatchedKMeans:
             Ks_np = np.ascontiguousarray(np.asarray(Ks, dtype=np.int32))
             g = int(grid or min(4 * cus, nh * len(Ks)))
             per = lambda gg: lib.cc_kmeans_f64_workspace_bytes(m, d, Ks_np.ctypes.data, len(Ks), gg)
-            while g > 1 and per(g) > self.workspace_budget:
+            # two resident workgroups per CU (the kernel's occupancy) whenever half the free
+            # device memory holds their scratch, even above workspace_budget: with one per CU the
+            # float64 fit runs ~1.25x longer (profiles/r04/f64_budget_r4ak.txt)
+            cap = max(self.workspace_budget, min(per(min(g, 2 * cus)), int(0.5 * torch.cuda.mem_get_info(dev)[0])))
+            while g > 1 and per(g) > cap:
                 g //= 2
             ws = workspace(dev, per(g))
             u, pos, stride = kpp_tables(Ks, self.n_init, self.seed, m, np.float64)
