@@ -73,7 +73,7 @@ struct F64Args {
   unsigned* counter;
   char* ws;
   size_t per_wg;
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf, o_cf;
 };
 
 // numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) of a contiguous double array:
@@ -223,7 +223,7 @@ __device__ unsigned long long cc_f64_stamps[16];
 #endif
 
 struct WG {
-  double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew, *xc, *xf;
+  double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew, *xc, *xf, *cf;
   int32_t *lab, *lold;
   uint8_t* lbest;
 };
@@ -249,7 +249,7 @@ __device__ __forceinline__ const double* xrow(const WG& w, int d, int r) { retur
 using f64x4 = __attribute__((ext_vector_type(4))) double;
 constexpr int MG = 4;  // k-steps per operand load group; two groups in flight
 
-template <int RT, int CT, int BS = 4>
+template <int RT, int CT, int BS = 4, int AS = 4>
 __device__ __forceinline__ void mfma_dots(const double* const (&pa)[CT], const double* const (&pb)[RT], int d,
                                           int q, f64x4 (&acc)[RT][CT]) {
 #pragma unroll
@@ -264,7 +264,7 @@ __device__ __forceinline__ void mfma_dots(const double* const (&pa)[CT], const d
     for (int i = 0; i < MG; ++i) {
       const int s = s0 + i < S ? s0 + i : S - 1;
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) a[i][ct] = pa[ct][4 * s];
+      for (int ct = 0; ct < CT; ++ct) a[i][ct] = pa[ct][AS * s];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) b[i][rt] = pb[rt][BS * s];
     }
@@ -293,7 +293,7 @@ __device__ __forceinline__ void mfma_dots(const double* const (&pa)[CT], const d
       const double bv = in ? pb[rt][BS * S] : 0.0;
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct)
-        acc[rt][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? pa[ct][4 * S] : 0.0, bv, acc[rt][ct], 0, 0, 0);
+        acc[rt][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? pa[ct][AS * S] : 0.0, bv, acc[rt][ct], 0, 0, 0);
     }
   }
 }
@@ -325,12 +325,10 @@ __device__ void estep_tiles(const WG& w, const double* cen, const double* cn, in
     for (int j0 = 0; j0 < K; j0 += 16 * CT) {
       const double* pa[CT];
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        const int j = j0 + 16 * ct + c16;
-        pa[ct] = cen + static_cast<size_t>(j < K ? j : K - 1) * d + q;
-      }
+      for (int ct = 0; ct < CT; ++ct)  // the centre tiles in the fragment image (zeros past K)
+        pa[ct] = w.cf + static_cast<size_t>((j0 >> 4) + ct) * ((d + 3) >> 2) * 64 + l;
       f64x4 acc[RT][CT];
-      mfma_dots<RT, CT, 64>(pa, pb, d, q, acc);
+      mfma_dots<RT, CT, 64, 64>(pa, pb, d, q, acc);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         double v = __builtin_inf();
@@ -360,7 +358,24 @@ __device__ void estep_tiles(const WG& w, const double* cen, const double* cn, in
   }
 }
 
+// the A-operand fragment image of nrow rows (row j: src[j], nullptr = zeros; rows up to a
+// multiple of 32): tile t, k-step s, lane l holds row 16t + (l & 15), feature 4s + (l >> 4)
+template <class Row>
+__device__ __forceinline__ void build_afrag(double* dst, Row row, int nrow, int d, int tid) {
+  const int S4 = (d + 3) >> 2;
+  const int ntl = ((nrow + 31) >> 5) * 2;
+  for (int e = tid; e < ntl * S4 * 64; e += NT) {
+    const int l = e & 63, ts = e >> 6;
+    const int t = ts / S4, sk = ts - t * S4;
+    const int j = 16 * t + (l & 15), k = 4 * sk + (l >> 4);
+    const double* src = j < nrow ? row(j) : nullptr;
+    dst[e] = (src && k < d) ? src[k] : 0.0;
+  }
+}
+
 __device__ __forceinline__ void estep_mfma(const WG& w, const double* cen, const double* cn, int K, int d, int m, int tid) {
+  build_afrag(w.cf, [&](int j) { return cen + static_cast<size_t>(j) * d; }, K, d, tid);
+  __syncthreads();
   if (K <= 16) estep_tiles<2, 1>(w, cen, cn, K, d, m, tid);
   else estep_tiles<2, 2>(w, cen, cn, K, d, m, tid);
   __syncthreads();
@@ -373,14 +388,16 @@ __device__ __forceinline__ void kpp_mfma(const WG& w, int d, int m, const int* c
   constexpr int RT = 2;
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int ntile = (m + 15) >> 4;
-  const double* pa[1] = {w.xc + static_cast<size_t>(cand[c16 < ntr ? c16 : ntr - 1]) * d + q};
+  build_afrag(w.cf, [&](int j) { return w.xc + static_cast<size_t>(cand[j]) * d; }, ntr, d, tid);
+  __syncthreads();
+  const double* pa[1] = {w.cf + l};
   for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
     const double* pb[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
       pb[rt] = w.xf + static_cast<size_t>(t0 + rt < ntile ? t0 + rt : ntile - 1) * ((d + 3) >> 2) * 64 + l;
     f64x4 acc[RT][1];
-    mfma_dots<RT, 1, 64>(pa, pb, d, q, acc);
+    mfma_dots<RT, 1, 64, 64>(pa, pb, d, q, acc);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int r = (t0 + rt) * 16 + c16;
@@ -670,6 +687,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   w.lbest = reinterpret_cast<uint8_t*>(base + a.o_lbest);
   w.xc = reinterpret_cast<double*>(base + a.o_xc);
   w.xf = reinterpret_cast<double*>(base + a.o_xf);
+  w.cf = reinterpret_cast<double*>(base + a.o_cf);
   const int m = a.m, d = a.d;
 #ifdef CC_F64_STAMPS
   // the accumulators in LDS (thread 0's registers would move the kernel's allocation)
@@ -1002,7 +1020,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
 }
 
 struct F64Layout {
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf, per_wg;
+  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf, o_cf, per_wg;
 };
 
 F64Layout f64_layout(int m, int d, int kmax) {
@@ -1021,6 +1039,7 @@ F64Layout f64_layout(int m, int d, int kmax) {
   L.o_lbest = o; o += al(m);
   L.o_xc = o;    o += al(sizeof(double) * static_cast<size_t>(m) * d);
   L.o_xf = o;    o += al(sizeof(double) * static_cast<size_t>((m + 15) / 16) * 16 * ((d + 3) / 4) * 4);
+  L.o_cf = o;    o += al(sizeof(double) * static_cast<size_t>((kmax + 31) / 32) * 32 * ((d + 3) / 4) * 4);
   L.per_wg = o;
   return L;
 }
@@ -1115,6 +1134,7 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.o_lbest = L.o_lbest;
   a.o_xc = L.o_xc;
   a.o_xf = L.o_xf;
+  a.o_cf = L.o_cf;
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nK));
   // one upload: the zeroed counter and the arguments (a pageable source is consumed before
   // hipMemcpyAsync returns)
