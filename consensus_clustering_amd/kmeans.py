@@ -232,8 +232,9 @@ class BatchedKMeans:
             # device memory holds their scratch, even above workspace_budget: with one per CU the
             # float64 fit runs ~1.25x longer (profiles/r04/f64_budget_r4ak.txt)
             cap = max(self.workspace_budget, min(per(min(g, 2 * cus)), int(0.5 * torch.cuda.mem_get_info(dev)[0])))
-            while g > 1 and per(g) > cap:
-                g //= 2
+            if per(g) > cap:  # the largest grid that fits (the scratch is linear in the grid)
+                unit = per(2) - per(1)
+                g = max(1, min(g, int((cap - (per(1) - unit)) // unit)))
             ws = workspace(dev, per(g))
             u, pos, stride = kpp_tables(Ks, self.n_init, self.seed, m, np.float64)
             u_d = torch.from_numpy(u).to(dev)
