@@ -38,7 +38,7 @@ import torch
 
 from . import dist, engine, post
 from ._hostfit import fit_predict_chunk, fit_predict_one
-from .kmeans import BatchedKMeans
+from .kmeans import DEFAULT_WORKSPACE_BUDGET, BatchedKMeans
 
 KMAX = 127  # largest K: uint8 labels (0xFF = not sampled) and int8 one-hot channels
 
@@ -84,7 +84,7 @@ class ConsensusClustering:
         *,
         keep_matrices='auto',
         device=None,
-        workspace_budget=40 << 30,
+        workspace_budget=DEFAULT_WORKSPACE_BUDGET,
         precision='auto',
         resampling='auto',
     ):
@@ -501,18 +501,29 @@ def host_fit_predict(clusterer, X, idx, n_jobs=1, parallelization_method='multit
     clusterer (the reference shares one, whose fit_predict can return another thread's labels).
     A process task carries a contiguous chunk of resamples (about four chunks per worker), and
     its function lives in a module that does not import torch (_hostfit), so a worker starts
-    with sklearn alone.  The labels do not depend on n_jobs."""
+    with sklearn alone.
+
+    'multithreading' runs a picklable clusterer on the same process pool: a host fit is GIL-bound
+    numpy glue for most foreign clusterers (GaussianMixture's EM measured 1.8x SLOWER on 16
+    joblib threads than serially, profiles/r04/rec_r4ai/gmm_time.txt), and the labels do not
+    depend on where a fit runs.  A clusterer that cannot be pickled stays on threads, each task
+    fitting its own clone.  The labels do not depend on n_jobs or the method as long as the
+    clusterer's randomness comes from its random_state, which _set_clusterer_K sets to the int
+    seed (CC.py:212) before every K."""
     H = len(idx)
     if H == 0:
-        return np.empty((0, 0), dtype=np.int32)
+        m = idx.shape[1] if getattr(idx, 'ndim', 1) == 2 else 0
+        return np.empty((0, m), dtype=np.int32)
     if n_jobs == 1:
         return np.stack([_fit_predict_one(clusterer, X[i]) for i in idx]).astype(np.int32)
     from joblib import Parallel, delayed, effective_n_jobs, parallel_config
 
-    if parallelization_method == 'multithreading':
+    if parallelization_method not in ('multithreading', 'multiprocessing'):
+        raise RuntimeError(f'unknown parallelization method: {parallelization_method}')
+    if parallelization_method == 'multithreading' and not _picklable(clusterer):
         out = Parallel(n_jobs=n_jobs, prefer='threads')(
             delayed(fit_predict_one)(_clone(clusterer), X[i]) for i in idx)
-    elif parallelization_method == 'multiprocessing':
+    else:
         chunks = max(1, min(H, 4 * effective_n_jobs(n_jobs)))
         bounds = np.linspace(0, H, chunks + 1).astype(int)
         # one BLAS thread per worker: loky would give each worker cpu_count // n_jobs threads,
@@ -523,9 +534,17 @@ def host_fit_predict(clusterer, X, idx, n_jobs=1, parallelization_method='multit
                 delayed(fit_predict_chunk)(clusterer, [X[i] for i in idx[a:b]])
                 for a, b in zip(bounds[:-1], bounds[1:]) if b > a)
         out = [lab for part in parts for lab in part]
-    else:
-        raise RuntimeError(f'unknown parallelization method: {parallelization_method}')
     return np.stack(out).astype(np.int32)
+
+
+def _picklable(obj):
+    import pickle
+
+    try:
+        pickle.dumps(obj)
+        return True
+    except Exception:
+        return False
 
 
 def _prepare(X, dev):

@@ -537,7 +537,8 @@ typedef int v8i __attribute__((ext_vector_type(8)));
 // One 16-B LDS-DMA piece per lane (global_load_lds_dwordx4: lane l lands at M0 + 16 l), issued
 // from inline asm with the wave-uniform LDS base in M0; completion is awaited explicitly with a
 // vmcnt(0) before the barrier that publishes the data.  No compiler-generated code in these
-// kernels uses M0.
+// kernels uses M0 (the backend reserves M0, so an "m0" clobber would be ignored); the CPU test
+// tests/test_isa.py checks that on the ISA of every kernel in libccmi.so.
 __device__ __forceinline__ void dma16(const void* g, const void* lds_base) {
   const unsigned la = static_cast<unsigned>(reinterpret_cast<uintptr_t>(
       (__attribute__((address_space(3))) const char*)lds_base));

@@ -10,6 +10,7 @@
 // Tiling: 64 x 64 output tiles of the upper triangle (the lower one is mirrored), 256 threads
 // as 16 x 16, each thread 4 x 4 pairs; 32-wide k slabs of both row blocks staged in LDS as
 // float32, [k][row] so that a thread reads its 4 rows and 4 columns with two 16-B reads.
+#include <tuple>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -413,7 +414,11 @@ __global__ __launch_bounds__(LT) void mst_kernel(const double* __restrict__ D, i
 // slice reads the merged column).  The barrier is a counter and a generation word in the
 // workspace, with agent-scope release / acquire fences (buffer_wbl2 / buffer_inv on gfx950, so
 // the D writes of one XCD are seen by the others); a workgroup that waits for more than ~2^27
-// polls sets an error word and every workgroup leaves (cc_linkage_check reports it).
+// polls sets an error word and every workgroup leaves (cc_linkage_check reports it).  The
+// workgroups are made co-resident, not assumed so: G is capped by the occupancy query of the
+// kernel at its dynamic LDS, and the grid forms are started with hipLaunchCooperativeKernel,
+// which the runtime starts only when all G workgroups can run at once; if it refuses, the
+// one-workgroup kernel runs instead (nothing has been written by then).
 constexpr int LG = 256;    // threads of a grid-form workgroup
 constexpr int GMAX = 128;  // workgroups of a grid form (all co-resident: one per CU at most)
 constexpr int NBG = 8;     // loads per thread in flight per slice pass
@@ -450,23 +455,27 @@ __device__ bool grid_sync(const GridWs& gw, unsigned& gen) {
     int ok = 1;
     const unsigned want = gen + 1;
     if constexpr (FULL) __threadfence();  // release (writes back this XCD's L2)
-    if (atomicAdd(&gw.bar[0], 1u) == gridDim.x - 1) {
-      atomicExch(&gw.bar[0], 0u);
+    // arrival and generation: release / acquire at agent scope (the slice minima of the light form
+    // are agent-scope atomics; these order them against the arrival and the generation word)
+    if (__hip_atomic_fetch_add(&gw.bar[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(&gw.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_s_waitcnt(0x0F70);  // the reset is done before the release
       if constexpr (FULL) __threadfence();
-      atomicExch(&gw.bar[1], want);
+      __hip_atomic_store(&gw.bar[1], want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       unsigned polls = 0;
       while (__hip_atomic_load(&gw.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
         __builtin_amdgcn_s_sleep(2);
         if ((++polls & 1023u) == 0) {
           if (__hip_atomic_load(&gw.bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || polls > (1u << 27)) {
-            atomicExch(&gw.bar[2], 1u);
+            __hip_atomic_store(&gw.bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ok = 0;
             break;
           }
         }
       }
+      // acquire: nothing after this reads before the generation word was seen
+      if (ok) (void)__hip_atomic_load(&gw.bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     }
     if constexpr (FULL) __threadfence();  // acquire (invalidates this CU's L1 and this XCD's L2)
     s_ok = ok;
@@ -714,16 +723,44 @@ size_t mask_bytes(int n) { return static_cast<size_t>((n + 31) >> 5) * sizeof(un
 constexpr size_t MASK_LDS_MAX = 160 * 1024 - 1024;
 
 // Workgroups of the grid forms for n (CCMI_LINK_G overrides; 0 = the one-workgroup kernels):
-// about 1536 entries per slice (six loads per thread), at most GMAX and one per CU.
-int link_groups(int n) {
+// about 1536 entries per slice (six loads per thread), at most GMAX and at most what the kernel's
+// occupancy at its dynamic LDS keeps resident on all CUs at once.
+template <typename Kern>
+int link_groups(int n, Kern kernel) {
   const char* e = std::getenv("CCMI_LINK_G");
   int cus = 0;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 1;
-  const int cap = std::max(1, std::min(GMAX, cus));
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel), LG,
+                                                   mask_bytes(n)) != hipSuccess)
+    per_cu = 0;
+  (void)hipGetLastError();
+  const int cap = std::min(GMAX, per_cu * cus);
+  if (cap <= 0) return 0;
   if (e && e[0]) return std::min(std::max(0, std::atoi(e)), cap);
   return std::max(1, std::min(cap, n / 1536));
+}
+
+// Start a grid form cooperatively (all G workgroups co-resident, or the launch fails); without
+// cooperative-launch support a plain launch of the occupancy-capped G.
+template <typename... KArgs, typename... Args>
+hipError_t launch_grid(void (*kernel)(KArgs...), int G, size_t lds, hipStream_t st, Args... args) {
+  int dev = 0, coop = 0;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && coop) {
+    std::tuple<KArgs...> a(args...);  // the kernel's own parameter types
+    void* argv[sizeof...(KArgs)];
+    std::apply([&argv](auto&... x) {
+      int k = 0;
+      ((argv[k++] = static_cast<void*>(&x)), ...);
+    }, a);
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kernel), dim3(G), dim3(LG), argv,
+                                      static_cast<unsigned>(lds), st);
+  }
+  hipLaunchKernelGGL(kernel, dim3(G), dim3(LG), lds, st, static_cast<KArgs>(args)...);
+  return hipGetLastError();
 }
 
 // Both forms: the barrier header (zeroed at every launch, so cc_linkage_check also reads a
@@ -736,11 +773,13 @@ size_t mst_ws(int n, int) { return grid_ws_bytes() + static_cast<size_t>(n) * si
 
 }  // namespace
 
-extern "C" size_t cc_linkage_workspace_bytes(int n) { return n > 0 ? nnchain_ws(n, link_groups(n)) : 0; }
+extern "C" size_t cc_linkage_workspace_bytes(int n) {
+  return n > 0 ? nnchain_ws(n, link_groups(n, nnchain_grid_kernel)) : 0;
+}
 
 extern "C" int cc_linkage_nnchain(double* D, int n, int method, double* Z, void* workspace, size_t ws_bytes,
                                   void* stream) {
-  const int G = n > 0 ? link_groups(n) : 0;
+  const int G = n > 0 ? link_groups(n, nnchain_grid_kernel) : 0;
   if (!D || !Z || n < 2 || !workspace || ws_bytes < nnchain_ws(n, G) ||
       (method != CC_LINK_AVERAGE && method != CC_LINK_COMPLETE && method != CC_LINK_WEIGHTED) ||
       mask_bytes(n) > MASK_LDS_MAX) {
@@ -754,12 +793,16 @@ extern "C" int cc_linkage_nnchain(double* D, int n, int method, double* Z, void*
     return CC_ERR_HIP;
   }
   int* sizes = reinterpret_cast<int*>(static_cast<char*>(workspace) + grid_ws_bytes());
-  if (G == 0)
+  e = hipErrorNotReady;
+  if (G > 0) {
+    e = launch_grid(nnchain_grid_kernel, G, mask_bytes(n), st, D, n, method, Z, sizes,
+                    sizes + static_cast<size_t>(G) * n, workspace);
+    if (e != hipSuccess) (void)hipGetLastError();  // refused before any workgroup ran
+  }
+  if (e != hipSuccess) {
     hipLaunchKernelGGL(nnchain_kernel, dim3(1), dim3(LT), mask_bytes(n), st, D, n, method, Z, sizes, sizes + n);
-  else
-    hipLaunchKernelGGL(nnchain_grid_kernel, dim3(G), dim3(LG), mask_bytes(n), st, D, n, method, Z, sizes,
-                       sizes + static_cast<size_t>(G) * n, workspace);
-  e = hipGetLastError();
+    e = hipGetLastError();
+  }
   if (e != hipSuccess) {
     cc::set_error(std::string("cc_linkage_nnchain: ") + hipGetErrorString(e));
     return CC_ERR_HIP;
@@ -767,10 +810,10 @@ extern "C" int cc_linkage_nnchain(double* D, int n, int method, double* Z, void*
   return CC_OK;
 }
 
-extern "C" size_t cc_linkage_mst_workspace_bytes(int n) { return n > 0 ? mst_ws(n, link_groups(n)) : 0; }
+extern "C" size_t cc_linkage_mst_workspace_bytes(int n) { return n > 0 ? mst_ws(n, link_groups(n, mst_grid_kernel)) : 0; }
 
 extern "C" int cc_linkage_mst(const double* D, int n, double* out, void* workspace, size_t ws_bytes, void* stream) {
-  const int G = n > 0 ? link_groups(n) : 0;
+  const int G = n > 0 ? link_groups(n, mst_grid_kernel) : 0;
   if (!D || !out || n < 2 || !workspace || ws_bytes < mst_ws(n, G) || mask_bytes(n) > MASK_LDS_MAX) {
     cc::set_error("cc_linkage_mst: bad arguments");
     return CC_ERR_ARG;
@@ -782,11 +825,15 @@ extern "C" int cc_linkage_mst(const double* D, int n, double* out, void* workspa
     return CC_ERR_HIP;
   }
   double* cur = reinterpret_cast<double*>(static_cast<char*>(workspace) + grid_ws_bytes());
-  if (G == 0)
+  e = hipErrorNotReady;
+  if (G > 0) {
+    e = launch_grid(mst_grid_kernel, G, mask_bytes(n), st, D, n, out, cur, workspace);
+    if (e != hipSuccess) (void)hipGetLastError();  // refused before any workgroup ran
+  }
+  if (e != hipSuccess) {
     hipLaunchKernelGGL(mst_kernel, dim3(1), dim3(LT), mask_bytes(n), st, D, n, out, cur);
-  else
-    hipLaunchKernelGGL(mst_grid_kernel, dim3(G), dim3(LG), mask_bytes(n), st, D, n, out, cur, workspace);
-  e = hipGetLastError();
+    e = hipGetLastError();
+  }
   if (e != hipSuccess) {
     cc::set_error(std::string("cc_linkage_mst: ") + hipGetErrorString(e));
     return CC_ERR_HIP;

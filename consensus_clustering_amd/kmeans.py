@@ -150,11 +150,14 @@ def prepare_rows(X, device):
     return Xd, xnorm, dpad, Xhl, int(e.value)
 
 
+DEFAULT_WORKSPACE_BUDGET = 40 << 30
+
+
 class BatchedKMeans:
     """All (h, K, init) k-means problems of a consensus fit, on one device."""
 
     def __init__(self, Ks, n_init=3, max_iter=300, tol=1e-4, random_state=0,
-                 workspace_budget=40 << 30, seedmax=None, wide_budget=96 << 30):
+                 workspace_budget=DEFAULT_WORKSPACE_BUDGET, seedmax=None, wide_budget=96 << 30):
         self.Ks = [int(k) for k in Ks]
         self.n_init = int(n_init)
         self.max_iter = int(max_iter)
@@ -228,10 +231,15 @@ class BatchedKMeans:
             Ks_np = np.ascontiguousarray(np.asarray(Ks, dtype=np.int32))
             g = int(grid or min(4 * cus, nh * len(Ks)))
             per = lambda gg: lib.cc_kmeans_f64_workspace_bytes(m, d, Ks_np.ctypes.data, len(Ks), gg)
-            # two resident workgroups per CU (the kernel's occupancy) whenever half the free
-            # device memory holds their scratch, even above workspace_budget: with one per CU the
-            # float64 fit runs ~1.25x longer (profiles/r04/f64_budget_r4ak.txt)
-            cap = max(self.workspace_budget, min(per(min(g, 2 * cus)), int(0.5 * torch.cuda.mem_get_info(dev)[0])))
+            # never more than half the free device memory.  At the DEFAULT budget the grid keeps two
+            # resident workgroups per CU (the kernel's occupancy) even when their scratch exceeds
+            # the budget: with one per CU the float64 fit runs ~1.25x longer
+            # (profiles/r04/f64_budget_r4ak.txt).  A budget the caller set is never exceeded.
+            free_half = int(0.5 * torch.cuda.mem_get_info(dev)[0])
+            if self.workspace_budget == DEFAULT_WORKSPACE_BUDGET:
+                cap = min(max(self.workspace_budget, per(min(g, 2 * cus))), free_half)
+            else:
+                cap = min(self.workspace_budget, free_half)
             if per(g) > cap:  # the largest grid that fits (the scratch is linear in the grid)
                 unit = per(2) - per(1)
                 g = max(1, min(g, int((cap - (per(1) - unit)) // unit)))

@@ -14,7 +14,7 @@ import torch
 from consensus_clustering_amd import engine
 from consensus_clustering_amd.kmeans import BatchedKMeans, prepare_rows
 from oracle import cc_oracle as O
-from tests.sk_parity import sklearn_parity
+from tests.sk_parity import sklearn_identical, sklearn_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -55,25 +55,18 @@ def run_gpu(X, Ks, H, frac, seed, n_init=3):
     (700, 2000, 4, [2, 4, 6], 3),
 ])
 def test_labels_match_sklearn(n, d, k_true, Ks, H):
-    from threadpoolctl import threadpool_limits
-
+    """sklearn's labels come from tests/golden/sk/lab_n<n>_d<d>.npz (make_sk_fixtures.py)."""
     seed = 7
+    case = f"lab_n{n}_d{d}"
     X = blobs(n, d, k_true, seed=n)
     idx, labs, inert, nit, stats = run_gpu(X, Ks, H, 0.8, seed)
     assert stats[0] > 0 and stats[2] > 0
-    with threadpool_limits(1):
-        for k, K in enumerate(Ks):
-            if K > k_true or n <= 100:
-                continue
-            for h in range(H):
-                ref = O.kmeans_labels(X[idx[h]], K, seed, n_init=3)
-                assert np.array_equal(ref, labs[k, h]), (K, h, np.mean(ref == labs[k, h]))
-    # every K: a disagreement only where sklearn's own float32 fit is rounding-sensitive.  Known
-    # gap of the wide engine (d > 128): at n=1200, d=300, K=8, h=2 it ends in a
-    # lower-inertia optimum (284 143) than any of sklearn's three inits (284 189 .. 284 431), and
-    # sklearn is stable under every perturbation sk_parity tries, including 22-bit k-means++
-    # distances (tools/emu_seed.py) and any tol; profiles/r03/parity_diag_wide_K8.txt
-    sklearn_parity(X, labs, idx, Ks, seed, resamples=H, threads=4, max_unexplained=1 if d > 128 else 0)
+    if n > 100:  # K <= k_true: identical to sklearn's float32 fit
+        assert sklearn_identical(case, X, labs, idx, max_K=k_true) > 0
+    # every K: a disagreement only where sklearn's own float32 fit is rounding-sensitive (sk_parity).
+    # Known gap of the wide engine (d > 128, DESIGN.md §4): at n=1200, d=300, K=8, h=2 it ends in a
+    # lower-inertia optimum (284 143) than any of sklearn's three inits (284 189 .. 284 431)
+    sklearn_parity(case, X, labs, idx, max_unexplained=1 if d > 128 else 0, Ks=Ks)
     assert np.all(nit >= 1) and np.all(nit <= 300)
     assert np.all(np.isfinite(inert))
 
@@ -208,7 +201,7 @@ def test_wide_expression_like():
     X = make_expression_f32(1000, 3000, seed=3)
     Ks, H, seed = [2, 3, 5, 7], 3, 0
     idx, labs, inert, nit, stats = run_gpu(X, Ks, H, 0.8, seed)
-    sklearn_parity(X, labs, idx, Ks, seed, resamples=H, threads=8)
+    sklearn_parity("expr_n1000_d3000", X, labs, idx, Ks=Ks)
     assert np.all(np.isfinite(inert))
 
 
@@ -258,6 +251,46 @@ def test_f64_labels_match_sklearn_float64(n, d, k_true, Ks, H):
                 ill += 1
     assert exact >= 0.9 * (exact + ill), (exact, ill)
 
+
+
+def test_f64_c3_shape_identical_to_sklearn_float64():
+    """float64 input at the C3 shape (n = 50 000, m = 40 000, d = 128, K = 2..20, 2 resamples;
+    VERDICT r4, next 3): cc_kmeans_f64's labels must be IDENTICAL to sklearn's float64
+    KMeans(n_init=3) for every (K, h), with the same n_iter; sklearn's side is the committed
+    fixture tests/golden/sk/f64_c3shape.npz (one thread in the development container)."""
+    from sklearn.datasets import make_blobs
+
+    from tests.conftest import digest
+    from tests.sk_parity import load_sk_fixture
+
+    f = load_sk_fixture("f64_c3shape")
+    meta = f["meta"]
+    X, _ = make_blobs(n_samples=50_000, n_features=128, centers=8, cluster_std=1.0,
+                      center_box=(-10, 10), shuffle=True, random_state=5)
+    assert digest(X) == meta["x_sha256"]
+    n, H, Ks, seed = meta["n"], meta["H"], meta["Ks"], meta["seed"]
+    m = int(meta["frac"] * n)
+    dev = engine.require_gpu()
+    idx = engine.resample_indices(seed, n, m, 0, H)
+    L = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
+    inert = torch.zeros((len(Ks), H), dtype=torch.float64, device=dev)
+    nit = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
+    BatchedKMeans(Ks, n_init=3, random_state=seed).run_f64(
+        torch.from_numpy(X).to(dev), torch.from_numpy(idx).to(dev), n, H, m, 0, H, L, inertia=inert, n_iter=nit)
+    torch.cuda.synchronize()
+    Lh = L.cpu().numpy()
+    nit, inert = nit.cpu().numpy(), inert.cpu().numpy()
+    bad, rel = [], 0.0
+    for k, K in enumerate(Ks):
+        for h in range(H):
+            got = Lh[k][idx[h], h].astype(np.int8)
+            if digest(got) != f["digest64"][k, h] or nit[k, h] != f["n_iter"][k, h]:
+                bad.append((K, h, int(nit[k, h]), int(f["n_iter"][k, h])))
+            rel = max(rel, abs(inert[k, h] - f["inertia"][k, h]) / f["inertia"][k, h])
+    print(f"f64 at the C3 shape: {len(Ks) * H - len(bad)}/{len(Ks) * H} label vectors and n_iter identical "
+          f"to sklearn float64; max relative inertia difference {rel:.2e}; differing {bad}")
+    assert not bad, bad
+    assert rel <= 1e-10, rel
 
 
 def _reloc_case(seed):
@@ -345,11 +378,9 @@ def test_sparse_mstep_against_dense(monkeypatch):
     problems that sk_parity cannot explain (a K > k_true problem with >= 99.9 % of its labels
     equal to sklearn's and an exact inertia within 7e-6 relative of sklearn's), and on the
     second seed both engines share it, so it is not the sparse M-step's: a known gap of the
-    f32-class engine.  Which rounding-sensitive cases sk_parity can explain
-    depends on the host's float32 BLAS kernels (sklearn runs on the GPU box's CPU): with the
-    same device labels, the sparse engine's (K = 14, h = 3) case (99.8 % of labels equal) was
-    explained by a 2^-22 nudge on earlier boxes and not on the box of profiles/r04/rec_r4ai, so
-    two per engine are allowed here."""
+    f32-class engine, allowed once per engine form.  sklearn's side is the committed
+    fixture tests/golden/sk/sparse_n4000_d128.npz, so the verdict does not depend on the GPU
+    box's float32 BLAS (on the box of profiles/r04/rec_r4ai it had, when sklearn ran there)."""
     n, d, k_true, Ks, H, seed = 4000, 128, 8, list(range(2, 15)), 4, 3
     X = blobs(n, d, k_true, seed=11)
     monkeypatch.delenv("CCMI_KM_DENSE", raising=False)
@@ -364,5 +395,6 @@ def test_sparse_mstep_against_dense(monkeypatch):
             assert all(same[k]), (K, same[k])
     ndiff = sum(not v for row in same for v in row)
     print(f"sparse vs dense M-step: {len(Ks) * H - ndiff}/{len(Ks) * H} label vectors identical")
-    sklearn_parity(X, sparse, idx, Ks, seed, resamples=H, threads=8, max_unexplained=2)
-    sklearn_parity(X, dense, idx, Ks, seed, resamples=H, threads=8, max_unexplained=2)
+    assert sklearn_identical("sparse_n4000_d128", X, sparse, idx, max_K=k_true) > 0
+    sklearn_parity("sparse_n4000_d128", X, sparse, idx, max_unexplained=1, Ks=Ks)
+    sklearn_parity("sparse_n4000_d128", X, dense, idx, max_unexplained=1, Ks=Ks)

@@ -112,6 +112,39 @@ def test_grid_linkage_equals_oracle(G, n, seed, ties, monkeypatch):
     np.testing.assert_array_equal(out.cpu().numpy(), O.mst_prim(D))
 
 
+def test_grid_linkage_while_another_stream_is_busy(monkeypatch):
+    """The grid forms started while another stream keeps the CUs busy (a chain of large GEMMs):
+    the cooperative launch makes the G workgroups co-resident instead of assuming it, so the
+    barriers cannot wait on a workgroup that never starts; the merges and edges still equal the
+    oracle's."""
+    monkeypatch.setenv("CCMI_LINK_G", "16")
+    n = 2000
+    D = _distances(n, 3, True)
+    want_z, want_p = O.nn_chain(D, "average"), O.mst_prim(D)
+    from consensus_clustering_amd import _lib
+
+    side = torch.cuda.Stream()
+    A = torch.randn(8192, 8192, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        for _ in range(12):
+            A = A @ A
+            A /= A.abs().max()
+    Z = engine.linkage_raw(torch.from_numpy(D).cuda(), "average").cpu().numpy()
+    with torch.cuda.stream(side):
+        for _ in range(12):
+            A = A @ A
+            A /= A.abs().max()
+    Dd = torch.from_numpy(D).cuda()
+    out = torch.empty((n - 1, 3), dtype=torch.float64, device="cuda")
+    ws = torch.empty(int(_lib.load().cc_linkage_mst_workspace_bytes(n)), dtype=torch.uint8, device="cuda")
+    _lib.call("cc_linkage_mst", Dd.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws.numel(), engine.stream_ptr())
+    _lib.call("cc_linkage_check", ws.data_ptr(), ws.numel(), engine.stream_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(Z, want_z)
+    np.testing.assert_array_equal(out.cpu().numpy(), want_p)
+
+
 def test_predict_single_linkage_equals_sklearn():
     """predict() with agg_clustering_linkage='single' (CC.py:306-312: AgglomerativeClustering(
     linkage='single', affinity='manhattan') on the rows of C) on the device: identical labels to

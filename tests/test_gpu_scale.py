@@ -23,7 +23,7 @@ import torch
 from bench import CONFIGS, SEED, make_blobs_f32, make_expression_f32
 from consensus_clustering_amd import engine, post
 from oracle import cc_oracle as O
-from tests.sk_parity import sklearn_parity
+from tests.sk_parity import sklearn_identical, sklearn_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -154,20 +154,9 @@ def check_tiles(cfg, cc, Ks_check=None):
                                           err_msg=f"tile {(bi, bj)} K={K}")
 
 
-def check_kmeans(cfg, X, cc, resamples):
-    from threadpoolctl import threadpool_limits
-
-    L = cc.labels_
-    idx = cc.resampling_indices_
-    with threadpool_limits(16):
-        for k, K in enumerate(cfg["Ks"]):
-            if K > cfg["k_true"]:
-                continue
-            col = L[k].cpu().numpy()
-            for h in range(resamples):
-                ref = O.kmeans_labels(X[idx[h]], K, SEED, n_init=3)
-                got = col[idx[h], h].astype(np.int64)
-                assert np.array_equal(ref, got), (K, h, float(np.mean(ref == got)))
+def check_kmeans(case, cfg, X, cc):
+    """K <= k_true: the labels of the fixture's resamples equal sklearn's float32 fit exactly."""
+    assert sklearn_identical(case, X, cc.labels_, cc.resampling_indices_, max_K=cfg["k_true"]) > 0
 
 
 def test_c4_full_size():
@@ -180,7 +169,7 @@ def test_c4_full_size():
     check_tiles(cfg, cc, Ks_check=[2, 5, 12])
     # the wide engine's known gap: at most one unexplained problem (K = 8, resample
     # 0: 1 row of 4 000 differs from sklearn)
-    sklearn_parity(X, cc.labels_, cc.resampling_indices_, cfg["Ks"], SEED, resamples=1, max_unexplained=1)
+    sklearn_parity("c4_full", X, cc.labels_, cc.resampling_indices_, max_unexplained=1, Ks=cfg["Ks"])
 
 
 def test_c3_full_size():
@@ -188,8 +177,8 @@ def test_c3_full_size():
     check_counts_sum(cfg, cc)
     check_labels(cfg, cc)
     check_tiles(cfg, cc, Ks_check=[2, 8, 13, 20])
-    check_kmeans(cfg, X, cc, resamples=2)
-    sklearn_parity(X, cc.labels_, cc.resampling_indices_, cfg["Ks"], SEED, resamples=1, skip=2)
+    check_kmeans("c3_full", cfg, X, cc)
+    sklearn_parity("c3_full", X, cc.labels_, cc.resampling_indices_, Ks=cfg["Ks"])
 
 
 def test_c5_full_size():
@@ -203,8 +192,8 @@ def test_c2_full_size_with_matrices():
     cfg, X, cc = fit_config("c2", keep=True)
     check_counts_sum(cfg, cc)
     check_labels(cfg, cc)
-    check_kmeans(cfg, X, cc, resamples=3)
-    sklearn_parity(X, cc.labels_, cc.resampling_indices_, cfg["Ks"], SEED, resamples=2, skip=3)
+    check_kmeans("c2_full", cfg, X, cc)
+    sklearn_parity("c2_full", X, cc.labels_, cc.resampling_indices_, Ks=cfg["Ks"])
     n = cfg["n"]
     idx = cc.resampling_indices_.astype(np.int64)
     I_ref = O.cosample_matrix(idx, n)

@@ -3,6 +3,7 @@ distances at the fast engine's operand precision) reproduces sklearn's own float
 well-posed problems, so that a disagreement it shows elsewhere is a rounding sensitivity, not an
 artefact of the restatement."""
 import numpy as np
+import pytest
 
 from tests.conftest import load_fixture
 from tests.sk_parity import kmeans_at_engine_precision
@@ -21,3 +22,36 @@ def test_engine_precision_emulation_reproduces_sklearn_when_well_posed():
                 for s in (4, 7):
                     got = kmeans_at_engine_precision(X[idx[h]], K, pf["meta"]["random_state"], 3, s=s)
                     np.testing.assert_array_equal(got, pf["labels"][j, h], err_msg=f"K={K} h={h} s={s}")
+
+
+def test_sk_fixture_classifier_on_its_own_labels():
+    """The fixture-based classifier (tests/golden/sk, make_sk_fixtures.py): sklearn's own labels
+    classify as identical, a recorded sklearn variant as explained, a permuted partition of an
+    insensitive problem as unexplained; the X recipe of the GPU test matches the fixture."""
+    from sklearn.datasets import make_blobs
+
+    from tests.sk_parity import load_sk_fixture, sklearn_identical, sklearn_parity
+
+    case = "sparse_n4000_d128"
+    f = load_sk_fixture(case)
+    meta = f["meta"]
+    X, _ = make_blobs(n_samples=4000, n_features=128, centers=8, cluster_std=1.0, center_box=(-10, 10),
+                      shuffle=True, random_state=11)
+    X = X.astype(np.float32)
+    n, hs, Ks = X.shape[0], meta["classify"], meta["Ks"]
+    idx = {h: np.random.RandomState(meta["seed"] + h).choice(n, int(0.8 * n), replace=False) for h in hs}
+    labels = [[f["ref32"][k, c].astype(np.int64) for c in range(len(hs))] for k in range(len(Ks))]
+    assert sklearn_identical(case, X, labels, idx) == len(Ks) * len(hs)
+    same, explained, total = sklearn_parity(case, X, labels, idx, Ks=Ks)
+    assert same == total and explained == 0
+    # an insensitive K > k_true problem with two rows' labels swapped: a neighbour of sklearn's
+    # partition, but sklearn is not rounding-sensitive there -> unexplained
+    k = next(k for k, K in enumerate(Ks) if K > 8 and f["reasons"][k, 0] == 0)
+    bad = [list(r) for r in labels]
+    lab = bad[k][0].copy()
+    i = int(np.flatnonzero(lab != lab[0])[0])
+    lab[0], lab[i] = lab[i], lab[0]
+    bad[k][0] = lab
+    with pytest.raises(AssertionError):
+        sklearn_parity(case, X, bad, idx, Ks=Ks)
+    sklearn_parity(case, X, bad, idx, Ks=Ks, max_unexplained=1)

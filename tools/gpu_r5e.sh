@@ -1,0 +1,9 @@
+# Stamps of diagnostic variants (C3 shape, H = 256): Lloyd-only full-sweep cycles
+set -o pipefail
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r5e; mkdir -p $O
+for v in ${VARS:-stamps}; do
+  KM_STAMPS_LIB=libccmi_$v.so timeout -k 10 200 python -u tools/km_stamps.py ${KM_H:-256} c3 > $O/st_$v.txt 2>&1 || { echo FAIL $v; tail -5 $O/st_$v.txt; exit 1; }
+  echo "== $v"; grep -v amdgpu.ids $O/st_$v.txt | grep -E "wave (0|4)|Lloyd-only|timings"
+done

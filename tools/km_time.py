@@ -25,20 +25,25 @@ m = int(cfg["frac"] * n)
 idx_d = torch.from_numpy(engine.resample_indices(SEED, n, m, 0, H)).to(dev)
 Xd, xn, _, Xhl, e = prepare_rows(X, dev)
 L = engine.new_label_matrix(len(cfg["Ks"]), n, engine.pad_h(H), dev)
+inert = torch.zeros((len(cfg["Ks"]), H), dtype=torch.float32, device=dev)
+nit = torch.zeros((len(cfg["Ks"]), H), dtype=torch.int32, device=dev)
 bk = BatchedKMeans(cfg["Ks"], n_init=3, random_state=SEED, max_iter=int(os.environ.get("KM_MAXITER", 300)),
                    workspace_budget=int(os.environ.get("KM_BUDGET_GB", 8)) << 30)
 ts = []
 for r in range(reps + 1):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    bk.run(Xd, xn, d, idx_d, n, H, m, 0, H, L, np.float32, Xhl=Xhl, scale_exp=e)
+    bk.run(Xd, xn, d, idx_d, n, H, m, 0, H, L, np.float32, Xhl=Xhl, scale_exp=e, inertia=inert, n_iter=nit)
     b.record()
     torch.cuda.synchronize()
     if r:
         ts.append(a.elapsed_time(b))
 print(os.path.basename(os.environ.get("CCMI_LIB", "libccmi.so")), "kmeans ms", [round(t, 1) for t in ts],
       "sweeps", int(bk.stats[4]), "sparse item-sweeps", int(bk.stats[6]), "changes", int(bk.stats[7]),
-      "labels sha", hashlib.sha256(L.cpu().numpy().tobytes()).hexdigest()[:16], flush=True)
+      "labels sha", hashlib.sha256(L.cpu().numpy().tobytes()).hexdigest()[:16],
+      "inertia sha", hashlib.sha256(inert.cpu().numpy().tobytes()).hexdigest()[:16],
+      "n_iter sha", hashlib.sha256(nit.cpu().numpy().tobytes()).hexdigest()[:16],
+      "ste sweeps", int(bk.stats[76]), flush=True)
 st = bk.stats.cpu().numpy()
 cyc, cnt = st[80:89].astype(float), st[96:105].astype(float)
 tot = max(cyc.sum(), 1)
