@@ -54,6 +54,12 @@ __global__ __launch_bounds__(64 * NWAVE) void bench(const float* Dsrc, unsigned 
       if (VAR == 1) grp1(v[u], 8 * u + 4 * hh, gm[u], gi[u]);
       else grp(v[u], 8 * u + 4 * hh, gm[u], gi[u]);
     }
+#if STAGE == 1
+    float sink = 0.f;
+    for (int u = 0; u < 8; ++u) sink += gm[u] + gi[u];
+    iacc[0] += sink;
+    continue;
+#endif
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const auto bs = __builtin_amdgcn_permlane32_swap(__float_as_uint(gm[u]), __float_as_uint(gm[u]), false, false);
@@ -61,6 +67,12 @@ __global__ __launch_bounds__(64 * NWAVE) void bench(const float* Dsrc, unsigned 
       om[u] = __uint_as_float(bs[1]);
       oi[u] = static_cast<int>(is[1]);
     }
+#if STAGE == 2
+    float sink = 0.f;
+    for (int u = 0; u < 8; ++u) sink += om[u] + oi[u];
+    iacc[0] += sink;
+    continue;
+#endif
     constexpr float INF = __builtin_huge_valf();
     float run = INF;
     int ri = 0, sbase = 0;
@@ -74,13 +86,16 @@ __global__ __launch_bounds__(64 * NWAVE) void bench(const float* Dsrc, unsigned 
       const bool lt = val < run;
       run = lt ? val : run;
       ri = lt ? vi : ri;
-      if ((emask >> G) & 1u) {
+      if (STAGE >= 4 && ((emask >> G) & 1u)) {
         if (hh == 0) {
           gl[G * 32 + ler] = static_cast<unsigned char>(ri - sbase);
           iacc[G] += run;
         }
       }
     }
+#if STAGE == 3
+    iacc[1] += run + ri;
+#endif
 #if NOBAR == 0
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
