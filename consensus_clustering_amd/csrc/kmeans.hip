@@ -910,23 +910,21 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
       for (int j0 = 0; j0 < h0; j0 += 4) amin_half<4, EAGER>(drow, base, j0, cnt, best, lab);  // 4 reads in flight
     }
     // merge the halves (v_permlane32_swap: lane i <-> i^32 without LDS): lower value, ties to
-    // the lower slot (half 0 holds the lower slots)
+    // the lower slot.  Half 0 holds the lower slots, so its lanes take the other half's minimum
+    // only when strictly lower and half 1's lanes on ties too: both halves end with the same
+    // (best, lab), and the stores below need no half-wave mask (both write the same byte)
     const auto bs = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
     const auto ls = __builtin_amdgcn_permlane32_swap(static_cast<unsigned>(lab), static_cast<unsigned>(lab), false, false);
     const float ob = __uint_as_float(hh ? bs[0] : bs[1]);
     const int ol = static_cast<int>(hh ? ls[0] : ls[1]);
-    if (ob < best || (ob == best && ol < lab)) {
-      best = ob;
-      lab = ol;
-    }
+    const bool upd = hh ? !(best < ob) : (ob < best);
+    best = upd ? ob : best;
+    lab = upd ? ol : lab;
     lab -= off + coff;
-    if (hh == 0) {
-      if (eok) {
-        glab[(static_cast<size_t>(2 * iw_prob(ww) + iw_buf(ww))) * a.lsm + erow] = static_cast<uint8_t>(lab);
-        es.iaccL[i] += xnr + best;
-      }
-      lsb[iw_prob(ww) * RT + ler] = eok ? static_cast<uint8_t>(lab) : 0xFF;  // M-step labels, by problem
-    }
+    const uint8_t lb = eok ? static_cast<uint8_t>(lab) : static_cast<uint8_t>(0xFF);  // 0xFF: rows past m
+    glab[(static_cast<size_t>(2 * iw_prob(ww) + iw_buf(ww))) * a.lsm + erow] = lb;
+    es.iaccL[i] += (eok && hh == 0) ? xnr + best : 0.f;
+    lsb[iw_prob(ww) * RT + ler] = lb;  // M-step labels, by problem
   }
 }
 

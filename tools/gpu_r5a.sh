@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r5a; mkdir -p $O
-timeout -k 10 900 python -u -m pytest -v --timeout 400 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest -v -s --timeout 400 --timeout-method thread \
   tests/test_gpu_kmeans.py tests/test_gpu_parity_blobs.py tests/test_gpu_linkage.py tests/test_gpu_scale.py -k "not c4_full" \
   > $O/tests.log 2>&1
 rc=$?
