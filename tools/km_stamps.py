@@ -38,7 +38,6 @@ cnt = st[96:105].astype(float)
 tot = max(cyc.sum(), 1)
 print("sweeps by active waves (1..8): count / share of sweep cycles / mean Mcycles:",
       {w: (int(cnt[w]), f"{100 * cyc[w] / tot:.0f}%", round(cyc[w] / max(cnt[w], 1) / 1e6, 2)) for w in range(1, 9)})
-cyc = st[106:115].astype(float)
-cnt = st[115:124].astype(float)
-print("Lloyd-only sweeps by width (1..8): count / share of ALL sweep cycles / mean Mcycles:",
-      {w: (int(cnt[w]), f"{100 * cyc[w] / tot:.0f}%", round(cyc[w] / max(cnt[w], 1) / 1e6, 2)) for w in range(1, 9)})
+pp = st[106:110] / 1e6
+print("post-processing phases (wg0, Mcycles): seeding %.1f, label compare %.1f, running sums %.1f, centre update %.1f"
+      % tuple(pp))

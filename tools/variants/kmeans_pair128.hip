@@ -96,6 +96,17 @@ template <int DP>
 constexpr bool kPair = KM_PAIR && DP <= 64;
 template <int DP>
 constexpr int kRing = kPair<DP> ? 8 : NRING;
+// d = 128 narrow pair mode (KM_PAIR128): sweeps of at most two slot tiles with no dense M-step run
+// two row tiles per interval, distance wave w on slot tile w & 1 of row tile 2p + (w >> 1), so
+// the four distance waves share what one or two of them carry alone in the per-tile loop.
+#ifndef KM_PAIR128
+#define KM_PAIR128 1
+#endif
+template <int DP>
+constexpr bool kPair128 = KM_PAIR128 && DP == 128;
+template <int DP>
+constexpr bool kPM = kPair<DP> || kPair128<DP>;  // the pair loops are compiled
+constexpr int kXN = 8;  // row-norm ring: the E-step of 2p-2, 2p-1 reads while 2p+2, 2p+3 land
 template <int DP>
 constexpr int kLsb = kPair<DP> ? 4 : 2;  // label buffers of the E-step -> M-step hand-off
 constexpr int US = CC_KM_USTRIDE;
@@ -194,6 +205,7 @@ struct State {
   int cand[PMAX][TMAX];
   // sweep
   int nitems, ncols;
+  int ndense;  // RUN items of the sweep with a dense M-step (one-hot MFMAs over the ring)
   unsigned char ikind[IMAX], iprob[IMAX], itr[IMAX];
   unsigned iw0[IMAX], iw1[IMAX];               // packed item words (see EState)
   unsigned char lstep[NW][NLS], sstep[NW][NSS][2];  // E-step steps of each wave (item; 0xFF none)
@@ -217,12 +229,6 @@ struct State {
   unsigned long long n_lloyd, n_seed, n_mrows, n_reloc, n_sweeps, n_ctiles, n_sparse, n_changes;
 };
 
-// Measured (round 5, C3): the sweep loops ran 7.5 % slower (1653 -> 1775 ms, identical results)
-// with the per-sweep item fields (ikind .. nsw) at offsets 0 mod 8 instead of 4 mod 8 -- a 4-byte
-// field added after ncols, or moved there, is enough; pads of 2 / 4 words were neutral.  New
-// State fields go to the end (a field there measured neutral).
-static_assert(offsetof(State, ikind) % 8 == 4, "State layout: see the note above");
-
 template <int DP>
 struct Lay {
   static constexpr int IMG = RT * DP * 2;     // one f16 image (hi or lo) of a tile, bytes
@@ -233,8 +239,8 @@ struct Lay {
   static constexpr int S_BYTES = CW * DP * 4;  // centre sums [CW][DP] f32, aliasing ring + D
   static_assert(S_BYTES <= U_END, "centre sums must fit in the ring + distance tiles");
   static constexpr int OFF_LS = (U_END + 32 + 15) / 16 * 16;  // labels [2][IMAX][RT] u8 (32 B slack: E-step over-reads)
-  static constexpr int OFF_XN = OFF_LS + kLsb<DP> * IMAX * RT;  // row norms [kRing][64] f32 (DMA'd, 32 used)
-  static constexpr int OFF_ST = OFF_XN + kRing<DP> * 64 * 4;
+  static constexpr int OFF_XN = OFF_LS + kLsb<DP> * IMAX * RT;  // row norms [kXN][64] f32 (DMA'd, 32 used)
+  static constexpr int OFF_ST = OFF_XN + kXN * 64 * 4;
   static constexpr int TOTAL = OFF_ST + ((sizeof(State) + 15) / 16) * 16;
   static_assert(TOTAL <= 163840, "LDS budget");
   static_assert(NSS % 4 == 0 && (NSS_D < 4 || NSS_D % 4 == 0), "seeding steps are read in batches");
@@ -868,8 +874,8 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
   // labels in buffer te & 3
   const int coff = PM ? 128 * (te & 1) : 0;
   const float* drow = Dt + (PM ? ((te >> 1) & 1) : (te & 1)) * (RT * DSD) + ler * DSD;
-  uint8_t* lsb = Ls + (PM ? (te & 3) : (te & 1)) * (IMAX * RT);
-  const float xnr = XN[(te % kRing<DP>) * 64 + ler];
+  uint8_t* lsb = Ls + (PM ? (te & (kLsb<DP> - 1)) : (te & 1)) * (IMAX * RT);
+  const float xnr = XN[(te % kXN) * 64 + ler];
   constexpr float INF = __builtin_huge_valf();
   // seeding steps first (one item per half-wave): descriptors and distances of every step in
   // flight together, then min with the closest distance, store for the potential and the next
@@ -1152,7 +1158,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_
     S.st[p] = ST_SEED;
     S.c[p] = 0;
   }
-  int ni = 0, nc = 0, nls = 0, nss2 = 0;  // items, slots, Lloyd steps, seeding half-steps
+  int ni = 0, nc = 0, nls = 0, nss2 = 0, nd = 0;  // items, slots, Lloyd steps, seeding half-steps, dense
   unsigned long long nseed = 0, nlloyd = 0, nm = 0;
   for (int p = 0; p < P; ++p) S.pitem[p] = -1;
   for (int p = 0; p < P; ++p) {
@@ -1206,6 +1212,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_
     // sparse: the sums follow the labels that changed (few moved in the last E-step; no M-step
     // MFMAs); dense: the M-step recomputes them (the first iteration, after a burst of changes)
     const bool sparse = sparse_ok && st == ST_RUN && S.pchg[p] <= a.m / 8;
+    nd += (st == ST_RUN && !sparse);
     S.isparse[ni] = static_cast<unsigned char>(sparse);
     S.ikind[ni] = static_cast<unsigned char>(kind);
     S.iprob[ni] = static_cast<unsigned char>(p);
@@ -1273,6 +1280,7 @@ __device__ void schedule(const KArgs& a, State& S, const int32_t* idx, int dist_
   }
   S.nitems = ni;
   S.ncols = nc;
+  S.ndense = nd;
   S.n_seed += nseed;
   S.n_lloyd += nlloyd;
   S.n_mrows += nm;
@@ -1409,7 +1417,9 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         S.sdesc[w][i][h] = seed_desc(a, S, S.sstep[w][i][h], T1);
       }
       const int hh = lane >> 5, lr = lane & 31;
-      const bool pm = kPair<DP> && ncols <= 4 * 32;  // block-uniform
+      // block-uniform: pair mode (d <= 64: up to four slot tiles; d = 128: up to two, no dense
+      // M-step, whose one-hot MFMAs would need the X tiles of two more intervals in the ring)
+      const bool pm = kPair<DP> ? ncols <= 4 * 32 : (kPair128<DP> && ncols <= 2 * 32 && S.ndense == 0);
       const int TP = (T + 1) >> 1;                    // row-tile pairs (pair mode)
 #ifdef CC_KM_STAMPS
       unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1420,11 +1430,13 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       // its own loop (one barrier per tile in both), so their register sets never overlap and
       // the vector chain of one role runs while the other role's MFMAs occupy the matrix pipe.
       if (wave < NDW) {
-        const int nsub = __builtin_amdgcn_readfirstlane(static_cast<int>(32 * wave < ncols) +
-                                                        static_cast<int>(32 * (wave + NDW) < ncols));
+        // this wave's slot tiles: w and w + NDW; in d = 128 pair mode w & 1 (of row tile 2p + (w >> 1))
+        const int fw = (kPair128<DP> && pm) ? (wave & 1) : wave;
+        const int nsub = __builtin_amdgcn_readfirstlane(static_cast<int>(32 * fw < ncols) +
+                                                        static_cast<int>(32 * (fw + NDW) < ncols));
         h8 ah0[DP / 16], al0[DP / 16], ah1[DP / 16], al1[DP / 16];
-        slot_frags<DP>(a, S, cen, 32 * wave + lr, ncols, hh, ah0, al0);
-        slot_frags<DP>(a, S, cen, 32 * (wave + NDW) + lr, ncols, hh, ah1, al1);
+        slot_frags<DP>(a, S, cen, 32 * fw + lr, ncols, hh, ah0, al0);
+        slot_frags<DP>(a, S, cen, 32 * (fw + NDW) + lr, ncols, hh, ah1, al1);
         // the distance wave's share of the E-steps (at most NLS_D Lloyd, NSS_D seeding steps)
         EState<NLS_D, NSS_D> es;
 #pragma unroll
@@ -1476,7 +1488,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           TileAddr<DP> An;
           tile_addr<DP>(a, nI, wave, lane, An);
           idx_issue<DP>(a, idx, (t + 2) * RT, wave, lane, nI);
-          if (t + 1 < T) tile_issue<DP>(An, ring + ((t + 1) % kRing<DP>) * LY::SLOT, XN + ((t + 1) % kRing<DP>) * 64, wave);
+          if (t + 1 < T) tile_issue<DP>(An, ring + ((t + 1) % kRing<DP>) * LY::SLOT, XN + ((t + 1) % kXN) * 64, wave);
           KM_STAMP(s2);
           {
             int tidl = tid;
@@ -1500,10 +1512,11 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           KM_ACC(4, s2e, s3);
           KM_ACC(5, s3, s4);
         }
-        } else if constexpr (kPair<DP>) {
+        } else if constexpr (kPM<DP>) {
           // pair mode: prologue tiles 0, 1 in the ring, indices of tiles 2, 3; per interval the
-          // distances of tiles 2p, 2p+1 (this wave's one slot tile, A fragments shared), the
-          // gather of 2p+2, 2p+3, the E-step share of 2p-2, 2p-1
+          // distances of tiles 2p, 2p+1 (d <= 64: this wave's one slot tile of both, A fragments
+          // shared; d = 128: slot tile w & 1 of tile 2p + (w >> 1)), the gather of 2p+2, 2p+3,
+          // the E-step share of 2p-2, 2p-1
           TileIdx<DP> nI0, nI1;
           unsigned preB[NSS_D];
 #pragma unroll
@@ -1525,21 +1538,29 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           }
           __syncthreads();
           for (int pr = 0; pr <= TP + 1; ++pr) {
+            KM_STAMP(s0);
             const int tA = 2 * pr, tB = tA + 1;
-            if (nsub == 1) {
+            if constexpr (kPair128<DP>) {
+              const int tm = tA + (wave >> 1);
+              if (nsub == 1 && tm < T)
+                dist_tiles<DP, 1>(a, S, ring + (tm % kRing<DP>) * LY::SLOT, Dt + (pr & 1) * (RT * DSD) + 128 * (wave >> 1),
+                                  wave & 1, lane, ah0, al0, ah1, al1);
+            } else if (nsub == 1) {
               float* dtile = Dt + (pr & 1) * (RT * DSD);
               if (tA < T) dist_tiles<DP, 1>(a, S, ring + (tA % kRing<DP>) * LY::SLOT, dtile, wave, lane, ah0, al0, ah1, al1);
               if (tB < T) dist_tiles<DP, 1>(a, S, ring + (tB % kRing<DP>) * LY::SLOT, dtile + 128, wave, lane, ah0, al0, ah1, al1);
             }
+            KM_STAMP(s1);
             TileAddr<DP> An0, An1;
             tile_addr<DP>(a, nI0, wave, lane, An0);
             tile_addr<DP>(a, nI1, wave, lane, An1);
             idx_issue<DP>(a, idx, (tA + 4) * RT, wave, lane, nI0);
             idx_issue<DP>(a, idx, (tA + 5) * RT, wave, lane, nI1);
             if (tA + 2 < T)
-              tile_issue<DP>(An0, ring + ((tA + 2) % kRing<DP>) * LY::SLOT, XN + ((tA + 2) % kRing<DP>) * 64, wave);
+              tile_issue<DP>(An0, ring + ((tA + 2) % kRing<DP>) * LY::SLOT, XN + ((tA + 2) % kXN) * 64, wave);
             if (tB + 2 < T)
-              tile_issue<DP>(An1, ring + ((tB + 2) % kRing<DP>) * LY::SLOT, XN + ((tB + 2) % kRing<DP>) * 64, wave);
+              tile_issue<DP>(An1, ring + ((tB + 2) % kRing<DP>) * LY::SLOT, XN + ((tB + 2) % kXN) * 64, wave);
+            KM_STAMP(s2);
             {
               int tidl = tid;
               asm volatile("" : "+v"(tidl));
@@ -1556,10 +1577,18 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
                 preB[i] = npreB[i];
               }
             }
+            KM_STAMP(s2e);
             dma_wait();  // tiles 2p+2, 2p+3 and the indices of 2p+4, 2p+5 have landed
             tile_addr_hold<DP>(An0);
             tile_addr_hold<DP>(An1);
+            KM_STAMP(s3);
             __syncthreads();
+            KM_STAMP(s4);
+            KM_ACC(1, s0, s1);
+            KM_ACC(0, s1, s2);
+            KM_ACC(2, s2, s2e);
+            KM_ACC(4, s2e, s3);
+            KM_ACC(5, s3, s4);
           }
         }
         estep_flush(S, tid, es);
@@ -1632,27 +1661,30 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           KM_ACC(3, s2, s3);
           KM_ACC(5, s3, s4);
         }
-        } else if constexpr (kPair<DP>) {
+        } else if constexpr (kPM<DP>) {
           // pair mode: per interval the E-steps of tiles 2p-2, 2p-1 and the M-steps of 2p-4,
-          // 2p-3, in tile order
+          // 2p-3, in tile order (d = 128: no M-step in a pair-mode sweep)
           unsigned preB[NSS];
 #pragma unroll
           for (int i = 0; i < NSS; ++i) preB[i] = 0;
           for (int pr = 0; pr <= TP + 1; ++pr) {
+            KM_STAMP(s0);
             const int tA = 2 * pr, tB = tA + 1;
             int tidl = tid;
             asm volatile("" : "+v"(tidl));
             unsigned npre[NSS], npreB[NSS];
             estep_prefetch<NSS>(a, S, tA, T, tidl, ns, dbuf, npre);
             estep_prefetch<NSS>(a, S, tB, T, tidl, ns, dbuf, npreB);
+            KM_STAMP(s1);
             estep<DP, NLS, NSS, true>(a, S, tA - 1, T, tidl, Dt, Ls, XN, glab, dbuf, pre, lw, nl, ns, es);
             if (((tA - 1) % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
             estep<DP, NLS, NSS, true>(a, S, tA, T, tidl, Dt, Ls, XN, glab, dbuf, preB, lw, nl, ns, es);
             if ((tA % FLUSH) == FLUSH - 1) estep_flush(S, tid, es);
+            KM_STAMP(s2);
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
               const int tm = tA - 4 + g;
-              if (tm >= 0 && tm < T && (mact0 || mact1)) {
+              if (kPair<DP> && tm >= 0 && tm < T && (mact0 || mact1)) {
                 const char* xs = ring + (tm % kRing<DP>) * LY::SLOT;
                 const uint8_t* lsb = Ls + (tm & 3) * (IMAX * RT);
                 mstep_tiles<DP, 2>(xs, lsb + myit0 * RT, lsb + myit1 * RT, lane, mycl0, mycl1, sacc0, sacc1, mcnt0, mcnt1, mact1);
@@ -1663,7 +1695,13 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
               pre[i] = npre[i];
               preB[i] = npreB[i];
             }
+            KM_STAMP(s3);
             __syncthreads();
+            KM_STAMP(s4);
+            KM_ACC(0, s0, s1);
+            KM_ACC(2, s1, s2);
+            KM_ACC(3, s2, s3);
+            KM_ACC(5, s3, s4);
           }
         }
         estep_flush(S, tid, es);
@@ -1674,7 +1712,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
       }
 #ifdef CC_KM_STAMPS
 #ifdef CC_KM_STAMPS_NARROW
-      if (ncols <= 32 && lane == 0 && a.stats)  // narrow sweeps only, every workgroup
+      if (ncols <= 64 && lane == 0 && a.stats)  // narrow sweeps only (<= 2 slot tiles), every workgroup
 #else
       if (blockIdx.x == 0 && lane == 0 && a.stats)
 #endif
@@ -1991,6 +2029,12 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
         const int wv = (ncols + 31) / 32;
         atomicAdd(&a.stats[80 + wv], pp1 - swp);
         atomicAdd(&a.stats[96 + wv], 1ull);
+        if (wv <= 2) {  // narrow sweeps: [110 + 3 * mode + wv] cycles, [119 + 3 * mode + wv] count
+          // mode 0: d = 128 pair mode, 1: per-tile with a dense M-step, 2: per-tile otherwise
+          const int mode = pm ? 0 : (S.ndense > 0 ? 1 : 2);
+          atomicAdd(&a.stats[110 + 3 * mode + wv], pp1 - swp);
+          atomicAdd(&a.stats[119 + 3 * mode + wv], 1ull);
+        }
       }
 #endif
     }
