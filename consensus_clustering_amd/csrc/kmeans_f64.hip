@@ -22,8 +22,12 @@
 // Dot products are sequential fused multiply-adds over the features (the BLAS micro-kernel
 // order); float contraction is otherwise off, as in the reference's compiled Cython.
 //
-// Mapping: a persistent grid; one 256-thread workgroup runs one (resample, K) unit at a time
-// (all its inits, sequentially), with per-workgroup float64 scratch in the caller's workspace.
+// Mapping: a persistent grid; one 256-thread workgroup runs one (resample, K) unit at a time,
+// units dealt in decreasing K, with per-workgroup float64 scratch in the caller's workspace.
+// Round 5: a unit's inits run in lockstep groups of up to GMAX (each pass over the rows - the
+// k-means++ distances, the E-step, the centre sums, the inertia - serves every running init of
+// the group; an init that converges leaves the group), and the centre sums accumulate in LDS
+// where they fit; every init's values and orders are those of a run on its own.
 // Round 4: the unit's centred rows are materialised once ([m][d] float64, the same subtraction),
 // every dot product runs as one of G (or ntr) independent sequential FMA chains per thread (a
 // thread's row against G centres at once: the same chain per value, G times the ILP), and the
@@ -42,6 +46,7 @@
 #include <cmath>
 #include <cstdint>
 #include <string>
+#include <type_traits>
 
 #include "ccmi_internal.h"
 
@@ -53,6 +58,7 @@ constexpr int NT = 256;
 constexpr int KMAX = 127;
 constexpr int TMAX = 6;
 constexpr int NKMAX = 64;
+constexpr int GMAX = 4;  // inits of a unit run in lockstep (groups of up to GMAX, in init order)
 
 struct F64Args {
   const double* X;  // [n][d] (not centred)
@@ -61,6 +67,7 @@ struct F64Args {
   int H, m, h_begin, nh;
   int nK;
   int Ks[NKMAX];
+  int korder[NKMAX];  // K indices by decreasing K: units are dealt heaviest first
   int n_init, max_iter;
   double tol_rel;
   const double* kpp_u;  // [nK][n_init][stride]
@@ -74,6 +81,7 @@ struct F64Args {
   char* ws;
   size_t per_wg;
   size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf, o_cf;
+  size_t kd, cfs;  // per-init strides (doubles) of the centres and of their operand images
 };
 
 // numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) of a contiguous double array:
@@ -222,15 +230,35 @@ __device__ unsigned long long cc_f64_stamps[16];
 #define F64_STAMP(ph)
 #endif
 
+// Per-init arrays are GMAX consecutive copies: cl / lab / lold [GMAX][m], dc [GMAX][TMAX][m],
+// cen / cnew [GMAX][kmax][d], cf [GMAX][cfs] (centre operand images).
 struct WG {
   double *mean, *xsq, *cl, *dc, *sq, *cen, *cnew, *xc, *xf, *cf;
   int32_t *lab, *lold;
   uint8_t* lbest;
+  int m;
+  size_t kd, cfs;
+  __device__ double* cl_of(int g) const { return cl + static_cast<size_t>(g) * m; }
+  __device__ double* dc_of(int g) const { return dc + static_cast<size_t>(g) * TMAX * m; }
+  __device__ int32_t* lab_of(int g) const { return lab + static_cast<size_t>(g) * m; }
+  __device__ int32_t* lold_of(int g) const { return lold + static_cast<size_t>(g) * m; }
+  __device__ double* cen_of(int g, int buf) const { return (buf ? cnew : cen) + static_cast<size_t>(g) * kd; }
+  __device__ double* cf_of(int g) const { return cf + static_cast<size_t>(g) * cfs; }
 };
 
 
 // The unit's centred row r (materialised: X[idx[r]][k] - mean[k], rounded once).
 __device__ __forceinline__ const double* xrow(const WG& w, int d, int r) { return w.xc + static_cast<size_t>(r) * d; }
+
+// Feature k of row r read from the fragment image (the same value as xrow(w, d, r)[k]): where a
+// thread walks its own row, the 16 rows of a tile sit in 128 contiguous bytes per feature, so a
+// wave's load touches 4 segments instead of 64 rows.
+struct XfRow {
+  const double* p;  // row r's lane in its tile
+  __device__ XfRow(const WG& w, int d, int r)
+      : p(w.xf + static_cast<size_t>(r >> 4) * ((d + 3) >> 2) * 64 + (r & 15)) {}
+  __device__ double operator[](int k) const { return p[(k >> 2) * 64 + 16 * (k & 3)]; }
+};
 
 // ---- float64 dot products on the matrix cores -------------------------------------------------
 // v_mfma_f64_16x16x4_f64 accumulates each of its outputs as the sequential fused multiply-add
@@ -307,57 +335,6 @@ __device__ __forceinline__ void lexmin(double& v, int& j, double v2, int j2) {
   }
 }
 
-// The E-step argmin of every row over the K centres: |c_j|^2 - 2 x.c_j (one rounding, as
-// sklearn's dgemm with beta = 1 on the centre norms), strict < over increasing j.  Each wave takes
-// RT row tiles of 16 at a time and the centres 16 * CT per pass; the running (distance, label) of
-// its rows stays in registers across passes.
-template <int RT, int CT>
-__device__ void estep_tiles(const WG& w, const double* cen, const double* cn, int K, int d, int m, int tid) {
-  const int l = tid & 63, q = l >> 4, c16 = l & 15;
-  const int ntile = (m + 15) >> 4;
-  for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
-    const double* pb[RT];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)  // the row tiles in the fragment image (past the last: clamped)
-      pb[rt] = w.xf + static_cast<size_t>(t0 + rt < ntile ? t0 + rt : ntile - 1) * ((d + 3) >> 2) * 64 + l;
-    double bv[RT];
-    int bj[RT];
-    for (int j0 = 0; j0 < K; j0 += 16 * CT) {
-      const double* pa[CT];
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct)  // the centre tiles in the fragment image (zeros past K)
-        pa[ct] = w.cf + static_cast<size_t>((j0 >> 4) + ct) * ((d + 3) >> 2) * 64 + l;
-      f64x4 acc[RT][CT];
-      mfma_dots<RT, CT, 64, 64>(pa, pb, d, q, acc);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        double v = __builtin_inf();
-        int jj = 0x7fffffff;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int j = j0 + 16 * ct + q + 4 * i;
-            if (j < K) lexmin(v, jj, __fma_rn(-2.0, acc[rt][ct][i], cn[j]), j);
-          }
-        lexmin(v, jj, __shfl_xor(v, 16), __shfl_xor(jj, 16));
-        lexmin(v, jj, __shfl_xor(v, 32), __shfl_xor(jj, 32));
-        if (j0 == 0) {
-          bv[rt] = v;
-          bj[rt] = jj;
-        } else {
-          lexmin(bv[rt], bj[rt], v, jj);
-        }
-      }
-    }
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int r = (t0 + rt) * 16 + c16;
-      if (q == 0 && r < m) w.lab[r] = bj[rt];
-    }
-  }
-}
-
 // the A-operand fragment image of nrow rows (row j: src[j], nullptr = zeros; rows up to a
 // multiple of 32): tile t, k-step s, lane l holds row 16t + (l & 15), feature 4s + (l >> 4)
 template <class Row>
@@ -373,48 +350,148 @@ __device__ __forceinline__ void build_afrag(double* dst, Row row, int nrow, int 
   }
 }
 
-__device__ __forceinline__ void estep_mfma(const WG& w, const double* cen, const double* cn, int K, int d, int m, int tid) {
-  build_afrag(w.cf, [&](int j) { return cen + static_cast<size_t>(j) * d; }, K, d, tid);
-  __syncthreads();
-  if (K <= 16) estep_tiles<2, 1>(w, cen, cn, K, d, m, tid);
-  else estep_tiles<2, 2>(w, cen, cn, K, d, m, tid);
-  __syncthreads();
-}
-
-// k-means++ distances to the candidate rows cand[0 .. ntr) (ntr <= 6, the first centre: ntr = 1):
-// ((-2 x.c) + |c|^2) + |x|^2 clipped at 0, then min with the closest distance so far (dc[t][r]),
-// or, for the first centre, the closest distances themselves (cl[r]).
-__device__ __forceinline__ void kpp_mfma(const WG& w, int d, int m, const int* cand, int ntr, bool first, int tid) {
-  constexpr int RT = 2;
+// par: bit g = which buffer holds init g's current centres (0: cen, 1: cnew)
+// The E-step argmin of every row over the K centres: |c_j|^2 - 2 x.c_j (one rounding, as
+// sklearn's dgemm with beta = 1 on the centre norms), strict < over increasing j (a (value, index)
+// lexicographic minimum: lowest index on ties).  Each wave takes RT row tiles of 16 at a time.  The
+// running inits of the lockstep group share the pass: their centres are packed into one operand
+// image (slot a = the a-th running init, row J = a K + j; no per-init padding to 16 rows), each
+// pass of 16 CT rows feeds every init's own running (distance, label) per row (gof[a]: the init of
+// slot a; a = floor((J + 0.5) / K) in float32 is exact: J + 0.5 is at least 0.5 / K from an
+// integer), and a row tile's B operands are read once for all the inits.
+template <int RT, int CT>
+__device__ void estep_packed(const WG& w, int na, const int* gof, const double* cn, int K, int d, int m, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int ntile = (m + 15) >> 4;
-  build_afrag(w.cf, [&](int j) { return w.xc + static_cast<size_t>(cand[j]) * d; }, ntr, d, tid);
-  __syncthreads();
-  const double* pa[1] = {w.cf + l};
+  const int nJ = na * K;
+  const float invK = 1.0f / static_cast<float>(K);
   for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
     const double* pb[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
       pb[rt] = w.xf + static_cast<size_t>(t0 + rt < ntile ? t0 + rt : ntile - 1) * ((d + 3) >> 2) * 64 + l;
-    f64x4 acc[RT][1];
-    mfma_dots<RT, 1, 64, 64>(pa, pb, d, q, acc);
+    double bv[RT][GMAX];
+    int bj[RT][GMAX];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int r = (t0 + rt) * 16 + c16;
-      if (r >= m) continue;
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {  // candidate t = q + 4i (< ntr <= 6)
-        const int t = q + 4 * i;
-        if (t >= ntr) continue;
-        double dd = -2.0 * acc[rt][0][i];
-        dd += w.xsq[cand[t]];
-        dd += w.xsq[r];
-        dd = dd > 0.0 ? dd : 0.0;
-        if (first) w.cl[r] = dd;
-        else w.dc[static_cast<size_t>(t) * m + r] = w.cl[r] < dd ? w.cl[r] : dd;
+      for (int a = 0; a < GMAX; ++a) {
+        bv[rt][a] = __builtin_inf();
+        bj[rt][a] = 0x7fffffff;
+      }
+    for (int J0 = 0; J0 < nJ; J0 += 16 * CT) {
+      const double* pa[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) pa[ct] = w.cf + static_cast<size_t>((J0 >> 4) + ct) * ((d + 3) >> 2) * 64 + l;
+      f64x4 acc[RT][CT];
+      mfma_dots<RT, CT, 64, 64>(pa, pb, d, q, acc);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int J = J0 + 16 * ct + q + 4 * i;
+          if (J >= nJ) continue;
+          const int a = static_cast<int>((static_cast<float>(J) + 0.5f) * invK);
+          const int j = J - a * K;
+          const double c2 = cn[gof[a] * (KMAX + 1) + j];
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) {
+            const double v = __fma_rn(-2.0, acc[rt][ct][i], c2);
+#pragma unroll
+            for (int aa = 0; aa < GMAX; ++aa)
+              if (aa == a) lexmin(bv[rt][aa], bj[rt][aa], v, j);
+          }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < GMAX; ++a) {
+      if (a >= na) break;
+      int32_t* lab = w.lab_of(gof[a]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        double v = bv[rt][a];
+        int jj = bj[rt][a];
+        lexmin(v, jj, __shfl_xor(v, 16), __shfl_xor(jj, 16));
+        lexmin(v, jj, __shfl_xor(v, 32), __shfl_xor(jj, 32));
+        const int r = (t0 + rt) * 16 + c16;
+        if (q == 0 && r < m) lab[r] = jj;
       }
     }
   }
+}
+
+// par: bit g = which buffer holds init g's current centres (0: cen, 1: cnew)
+__device__ __forceinline__ void estep_multi(const WG& w, unsigned act, unsigned par, int G, const double* cn, int K,
+                                            int d, int m, int* gof, int tid) {
+  int na = 0;
+  for (int g = 0; g < G; ++g)
+    if ((act >> g) & 1u) {
+      if (tid == 0) gof[na] = g;
+      ++na;
+    }
+  // the running inits' centres, packed: row J = a K + j is centre j of the a-th running init
+  build_afrag(w.cf, [&](int J) {
+    int a = 0, g = 0;
+    for (; g < G; ++g)
+      if ((act >> g) & 1u) {
+        if (a == J / K) break;
+        ++a;
+      }
+    return w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(J - (J / K) * K) * d;
+  }, na * K, d, tid);
+  __syncthreads();
+  if (na * K <= 16) estep_packed<2, 1>(w, na, gof, cn, K, d, m, tid);
+  else estep_packed<2, 2>(w, na, gof, cn, K, d, m, tid);
+  __syncthreads();
+}
+
+// k-means++ distances of a lockstep group: init g's candidates are cand[g * TMAX + t], t < ntr
+// (first centre: ntr = 1), all G * ntr <= 24 of them as the centres of one pass over the rows;
+// each value is kpp_mfma's ((-2 x.c) + |c|^2) + |x|^2 clipped at 0, min with init g's closest.
+__device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const int* cand, int ntr, int G, bool first,
+                                               int tid) {
+  constexpr int RT = 2;
+  const int l = tid & 63, q = l >> 4, c16 = l & 15;
+  const int ntile = (m + 15) >> 4;
+  const int nc = G * ntr;
+  build_afrag(w.cf, [&](int j) { return w.xc + static_cast<size_t>(cand[(j / ntr) * TMAX + j % ntr]) * d; }, nc, d, tid);
+  __syncthreads();
+  auto body = [&](auto ctc) __attribute__((always_inline)) {
+    constexpr int CT = decltype(ctc)::value;
+    const double* pa[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) pa[ct] = w.cf + static_cast<size_t>(ct) * ((d + 3) >> 2) * 64 + l;
+    for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
+      const double* pb[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        pb[rt] = w.xf + static_cast<size_t>(t0 + rt < ntile ? t0 + rt : ntile - 1) * ((d + 3) >> 2) * 64 + l;
+      f64x4 acc[RT][CT];
+      mfma_dots<RT, CT, 64, 64>(pa, pb, d, q, acc);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = (t0 + rt) * 16 + c16;
+        if (r >= m) continue;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int jj = 16 * ct + q + 4 * i;
+            if (jj >= nc) continue;
+            const int g = jj / ntr, t = jj - g * ntr;
+            double dd = -2.0 * acc[rt][ct][i];
+            dd += w.xsq[cand[g * TMAX + t]];
+            dd += w.xsq[r];
+            dd = dd > 0.0 ? dd : 0.0;
+            double* cl = w.cl_of(g);
+            if (first) cl[r] = dd;
+            else w.dc_of(g)[static_cast<size_t>(t) * m + r] = cl[r] < dd ? cl[r] : dd;
+          }
+      }
+    }
+  };
+  if (nc <= 16) body(std::integral_constant<int, 1>{});
+  else body(std::integral_constant<int, 2>{});
   __syncthreads();
 }
 
@@ -423,18 +500,20 @@ __device__ __forceinline__ void kpp_mfma(const WG& w, int d, int m, const int* c
 // one-hot labels: lane l cluster l & 15, row 4s + (l >> 4); B = the rows: lane l feature l & 15).
 // fma(1, x, acc) = acc + x is sklearn's addition (centers_new[j] += x * 1.0); fma(0, x, acc) =
 // acc + (+-0) = acc exactly for finite x, the accumulators starting at +0 and never -0 - so each
-// output is the row-order sum of its cluster's rows, as the list walk computed it.  A wave owns
-// CTP cluster tiles x FTP 16-feature tiles per pass over the rows; the passes cover the rows'
-// feature slices once.
-// FTP feature tiles per pass: FTP independent chains per cluster tile (the issue of one chain's
-// dependent MFMAs alone leaves the matrix core idle).
+// output is the row-order sum of its cluster's rows.  A wave owns CTP cluster tiles x FTP
+// 16-feature tiles per pass over the rows.  The running inits of the lockstep group share the pass:
+// their clusters are packed (slot a = the a-th running init, cluster row J = a K + j, so one tile
+// may hold clusters of two inits; lane l's A operand reads the labels of its own cluster's init),
+// and the B operands (the rows) are loaded once per k-step for all of them.
 template <int CTP, int FTP>
-__device__ void msum_tiles(const WG& w, double* cnew, int K, int d, int m, int tid) {
+__device__ void msum_packed(const WG& w, unsigned par, int na, const int* gof, int K, int d, int m, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
-  const int nct = (K + 15) >> 4, nft = (d + 15) >> 4;
+  const int nJ = na * K;
+  const int nct = (nJ + 15) >> 4, nft = (d + 15) >> 4;
   const int nfg = (nft + FTP - 1) / FTP;
   const int ncg = (nct + CTP - 1) / CTP;
   const int S = (m + 3) >> 2;
+  const float invK = 1.0f / static_cast<float>(K);
   for (int item = tid >> 6; item < ncg * nfg; item += NT / 64) {
     const int cg = item / nfg, fg = item - cg * nfg;
     int f[FTP];
@@ -444,35 +523,42 @@ __device__ void msum_tiles(const WG& w, double* cnew, int K, int d, int m, int t
       f[u] = (fg * FTP + u) * 16 + c16;
       pb[u] = w.xc + (f[u] < d ? f[u] : d - 1) + static_cast<size_t>(q) * d;
     }
-    const int32_t* pl = w.lab + q;
+    // lane's A-operand cluster of each tile: packed row J -> (init, cluster); past nJ: none
     int jl[CTP];
-    f64x4 acc[CTP][FTP];
+    const int32_t* pl[CTP];
 #pragma unroll
     for (int ct = 0; ct < CTP; ++ct) {
-      jl[ct] = (cg * CTP + ct) * 16 + c16;
+      const int J = (cg * CTP + ct) * 16 + c16;
+      const int a = J < nJ ? static_cast<int>((static_cast<float>(J) + 0.5f) * invK) : 0;
+      jl[ct] = J < nJ ? J - a * K : -2;
+      pl[ct] = w.lab_of(gof[a]) + q;
+    }
+    f64x4 acc[CTP][FTP];
+#pragma unroll
+    for (int ct = 0; ct < CTP; ++ct)
 #pragma unroll
       for (int u = 0; u < FTP; ++u) acc[ct][u] = f64x4{0.0, 0.0, 0.0, 0.0};
-    }
-    int lb0[MG], lb1[MG];
+    int lb0[MG][CTP], lb1[MG][CTP];
     double b0[MG][FTP], b1[MG][FTP];
-    auto ld = [&](int (&lv)[MG], double (&bv)[MG][FTP], int s0) __attribute__((always_inline)) {
+    auto ld = [&](int (&lv)[MG][CTP], double (&bv)[MG][FTP], int s0) __attribute__((always_inline)) {
       if (s0 >= S) return;
 #pragma unroll
       for (int i = 0; i < MG; ++i) {
         const int r = 4 * (s0 + i) + q;
         const bool in = s0 + i < S && r < m;
-        lv[i] = in ? pl[4 * (s0 + i)] : -1;
+#pragma unroll
+        for (int ct = 0; ct < CTP; ++ct) lv[i][ct] = in ? pl[ct][4 * (s0 + i)] : -1;
 #pragma unroll
         for (int u = 0; u < FTP; ++u) bv[i][u] = in ? pb[u][static_cast<size_t>(4 * (s0 + i)) * d] : 0.0;
       }
     };
-    auto mm = [&](const int (&lv)[MG], const double (&bv)[MG][FTP], int s0) __attribute__((always_inline)) {
+    auto mm = [&](const int (&lv)[MG][CTP], const double (&bv)[MG][FTP], int s0) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < MG; ++i)
         if (s0 + i < S)
 #pragma unroll
           for (int ct = 0; ct < CTP; ++ct) {
-            const double av = lv[i] == jl[ct] ? 1.0 : 0.0;
+            const double av = lv[i][ct] == jl[ct] ? 1.0 : 0.0;
 #pragma unroll
             for (int u = 0; u < FTP; ++u)
               acc[ct][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv[i][u], acc[ct][u], 0, 0, 0);
@@ -492,22 +578,25 @@ __device__ void msum_tiles(const WG& w, double* cnew, int K, int d, int m, int t
         for (int ct = 0; ct < CTP; ++ct)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int j = (cg * CTP + ct) * 16 + q + 4 * i;
-            if (j < K) cnew[static_cast<size_t>(j) * d + f[u]] = acc[ct][u][i];
+            const int J = (cg * CTP + ct) * 16 + q + 4 * i;
+            if (J >= nJ) continue;
+            const int a = static_cast<int>((static_cast<float>(J) + 0.5f) * invK);
+            const int g = gof[a];
+            double* cnew = w.cen_of(g, ((par >> g) & 1u) ^ 1u);
+            cnew[static_cast<size_t>(J - a * K) * d + f[u]] = acc[ct][u][i];
           }
   }
 }
 
-// two feature tiles (two more independent chains) per wave where every wave still gets a pass
-__device__ __forceinline__ void msum_mfma(const WG& w, double* cnew, int K, int d, int m, int tid) {
-  const bool two = ((d + 31) >> 5) * (K <= 16 ? 1 : (((K + 15) >> 4) + 1) / 2) >= NT / 64;
-  if (K <= 16) {
-    if (two) msum_tiles<1, 2>(w, cnew, K, d, m, tid);
-    else msum_tiles<1, 1>(w, cnew, K, d, m, tid);
-  } else {
-    if (two) msum_tiles<2, 2>(w, cnew, K, d, m, tid);
-    else msum_tiles<2, 1>(w, cnew, K, d, m, tid);
-  }
+// the packed E-step's slot map must be current (estep_multi wrote gof for the same act)
+__device__ __forceinline__ void msum_multi(const WG& w, unsigned par, int na, const int* gof, int K, int d, int m,
+                                           int tid) {
+  const int nct = (na * K + 15) >> 4, nft = (d + 15) >> 4;
+  // as many cluster tiles per wave as keep every wave busy: each cluster-tile group re-reads the
+  // rows, and the passes over the rows are what the sums wait on
+  if (nct >= 3 && ((nct + 3) / 4) * nft >= NT / 64) msum_packed<4, 1>(w, par, na, gof, K, d, m, tid);
+  else if (nct >= 2 && ((nct + 1) / 2) * nft >= NT / 64) msum_packed<2, 1>(w, par, na, gof, K, d, m, tid);
+  else msum_packed<1, 1>(w, par, na, gof, K, d, m, tid);
   __syncthreads();
 }
 
@@ -518,66 +607,83 @@ __device__ __forceinline__ void msum_mfma(const WG& w, double* cnew, int K, int 
 // workgroup (the BLAS potentials, whose accumulators are independent until their final folds).
 constexpr int CB = 1024;  // search staging block (doubles); the LDS area holds 2 * CB
 
-// cand[t] = searchsorted(cumsum(cl), u[t] * pot) clipped to m - 1, t < ntr.  Thread 0 runs the
-// float64 cumulative sum in row order over LDS blocks (the workgroup stages the next block
-// meanwhile); the running sum is non-decreasing, so the thresholds, sorted, are crossed in order.
-__device__ void kpp_search(const WG& w, int m, const double* u, double pot, int ntr, int* cand,
-                           double* sb, int* sflag, double* s_thr, int* s_tix, int tid) {
-  if (tid == 0) {
+// kpp_search for every init of a lockstep group at once: init g's walk runs on the first thread
+// of wave g (the walks of different inits overlap), each over its own staged blocks of CBM values
+// (sb: [GMAX][2][CBM]).  Init g: cand[g TMAX + t] = searchsorted(cumsum(cl_g), u[g][t] pot[g])
+// clipped to m - 1, t < ntr: the float64 cumulative sum in row order, 8 partial sums then one
+// comparison with the next of the sorted thresholds (the sums do not decrease, so the
+// thresholds are crossed in order).
+constexpr int CBM = 512;
+__device__ void kpp_search_multi(const WG& w, int G, int m, const double* const (&u)[GMAX], const double (&pot)[GMAX],
+                                 int ntr, int* cand, double* sb, int* sflag, double* s_thr, int* s_tix, int tid) {
+  const int wv = tid >> 6;
+  const bool walker = (tid & 63) == 0 && wv < G;
+  if (walker) {
+    double* thr = s_thr + wv * TMAX;
+    int* tix = s_tix + wv * TMAX;
     for (int t = 0; t < ntr; ++t) {
-      s_thr[t] = u[t] * pot;
-      s_tix[t] = t;
+      thr[t] = u[wv][t] * pot[wv];
+      tix[t] = t;
     }
     for (int t = 1; t < ntr; ++t)  // insertion sort of the thresholds (ties: either order)
-      for (int v = t; v > 0 && s_thr[v] < s_thr[v - 1]; --v) {
-        const double x = s_thr[v];
-        s_thr[v] = s_thr[v - 1];
-        s_thr[v - 1] = x;
-        const int y = s_tix[v];
-        s_tix[v] = s_tix[v - 1];
-        s_tix[v - 1] = y;
+      for (int v = t; v > 0 && thr[v] < thr[v - 1]; --v) {
+        const double x = thr[v];
+        thr[v] = thr[v - 1];
+        thr[v - 1] = x;
+        const int y = tix[v];
+        tix[v] = tix[v - 1];
+        tix[v - 1] = y;
       }
-    for (int t = 0; t < ntr; ++t) cand[t] = m - 1;  // not crossed: clipped to m - 1
-    *sflag = 0;
+    for (int t = 0; t < ntr; ++t) cand[wv * TMAX + t] = m - 1;  // not crossed: clipped to m - 1
+    sflag[wv] = 0;
   }
-  for (int e = tid; e < CB && e < m; e += NT) sb[e] = w.cl[e];
+  for (int e = tid; e < G * CBM; e += NT) {
+    const int g = e / CBM, i = e - g * CBM;
+    if (i < m) sb[g * 2 * CBM + i] = w.cl_of(g)[i];
+  }
   __syncthreads();
-  double cum = 0.0, tn = s_thr[0];
+  double cum = 0.0, tn = walker ? s_thr[wv * TMAX] : 0.0;
   int next = 0;
   int buf = 0;
-  for (int b0 = 0; b0 < m; b0 += CB) {
-    const int nb = b0 + CB;
-    double* nxt = sb + (buf ^ 1) * CB;
-    for (int e = tid; e < CB && nb + e < m; e += NT) nxt[e] = w.cl[nb + e];
-    if (tid == 0) {
-      const double* cur = sb + buf * CB;
-      const int n = m - b0 < CB ? m - b0 : CB;
+  for (int b0 = 0; b0 < m; b0 += CBM) {
+    const int nb = b0 + CBM;
+    for (int e = tid; e < G * CBM; e += NT) {
+      const int g = e / CBM, i = e - g * CBM;
+      if (nb + i < m) sb[(g * 2 + (buf ^ 1)) * CBM + i] = w.cl_of(g)[nb + i];
+    }
+    if (walker && !sflag[wv]) {
+      const double* cur = sb + (wv * 2 + buf) * CBM;
+      const double* thr = s_thr + wv * TMAX;
+      const int* tix = s_tix + wv * TMAX;
+      const int n = m - b0 < CBM ? m - b0 : CBM;
       for (int i0 = 0; i0 < n && next < ntr; i0 += 8) {
         // 8 partial sums, then one comparison with the next threshold (the sums do not decrease)
         double cs[8];
-        const int g = n - i0 < 8 ? n - i0 : 8;
+        const int g8 = n - i0 < 8 ? n - i0 : 8;
         double c = cum;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          if (i < g) c += cur[i0 + i];
+          if (i < g8) c += cur[i0 + i];
           cs[i] = c;
         }
         if (!(c < tn)) {
 #pragma unroll
           for (int i = 0; i < 8; ++i)
-            while (i < g && next < ntr && !(cs[i] < tn)) {
+            while (i < g8 && next < ntr && !(cs[i] < tn)) {
               const int p = b0 + i0 + i;
-              cand[s_tix[next]] = p < m - 1 ? p : m - 1;
+              cand[wv * TMAX + tix[next]] = p < m - 1 ? p : m - 1;
               ++next;
-              tn = next < ntr ? s_thr[next] : 0.0;
+              tn = next < ntr ? thr[next] : 0.0;
             }
         }
         cum = c;
       }
-      if (next >= ntr) *sflag = 1;
+      if (next >= ntr) sflag[wv] = 1;
     }
     __syncthreads();
-    if (*sflag) break;
+    int all = 1;
+    for (int g = 0; g < G; ++g) all &= sflag[g];
+    if (all) break;
     buf ^= 1;
   }
   __syncthreads();
@@ -597,49 +703,54 @@ __device__ __forceinline__ double chain_sum(const double* x, int i0, int e, int 
   return acc;
 }
 
-// s_pot[t] = blas_gemv_t_ones(dc + t m, m, t, ntr) for t < ntr, its (column, 2048-row block, lane)
-// accumulator chains one per thread (part: an LDS area of 2 * CB doubles), the folds by thread t
-__device__ void kpp_pots(const WG& w, int m, int ntr, double* part, double* pot, int tid) {
+// The candidates' potentials for every init of a lockstep group at once: pot[g TMAX + t] =
+// blas_gemv_t_ones(column (g, t) = w.dc_of(g) + t m, m, t, ntr), its (column, 2048-row block,
+// lane) accumulator chains one per thread, the folds by thread g ntr + t.
+__device__ void kpp_pots_multi(const WG& w, int G, int m, int ntr, double* part, double* pot, int tid) {
   const int n4 = ntr & ~3, rem = ntr - n4;
   const int m1 = m & ~3;
   const int nb = (m1 + 2047) / 2048;
-  const int G = (2 * CB) / (ntr * 4);  // blocks per round
+  const int nc = G * ntr;
+  const int GB = (2 * CB) / (nc * 4);  // blocks per round
   double y = 0.0;
-  for (int bb = 0; bb < nb; bb += G) {
-    const int gb = nb - bb < G ? nb - bb : G;
-    for (int ch = tid; ch < ntr * gb * 4; ch += NT) {
-      const int t = ch / (gb * 4), g = (ch >> 2) % gb, q = ch & 3;
+  for (int bb = 0; bb < nb; bb += GB) {
+    const int gb = nb - bb < GB ? nb - bb : GB;
+    for (int ch = tid; ch < nc * gb * 4; ch += NT) {
+      const int c = ch / (gb * 4), g = (ch >> 2) % gb, q = ch & 3;
+      const int t = c % ntr;
       const int L = (rem >= 2 && t >= n4 && t < n4 + 2) ? 2 : 4;
       if (q >= L) continue;
       const int b = (bb + g) * 2048, e = b + 2048 < m1 ? b + 2048 : m1;
-      part[(t * G + g) * 4 + q] = chain_sum(w.dc + static_cast<size_t>(t) * m, b + q, e, L);
+      part[(c * GB + g) * 4 + q] = chain_sum(w.dc_of(c / ntr) + static_cast<size_t>(t) * m, b + q, e, L);
     }
     __syncthreads();
-    if (tid < ntr) {
-      const bool two = rem >= 2 && tid >= n4 && tid < n4 + 2;
+    if (tid < nc) {
+      const int t = tid % ntr;
+      const bool two = rem >= 2 && t >= n4 && t < n4 + 2;
       for (int g = 0; g < gb; ++g) {
-        const double* pp = part + (tid * G + g) * 4;
+        const double* pp = part + (tid * GB + g) * 4;
         y += two ? pp[0] + pp[1] : (pp[0] + pp[2]) + (pp[1] + pp[3]);
       }
     }
     __syncthreads();
   }
-  if (tid < ntr) {
+  if (tid < nc) {
+    const int t = tid % ntr;
     if (m1 < m) {
-      const double* x = w.dc + static_cast<size_t>(tid) * m;
-      double t = x[m1];
-      for (int i = m1 + 1; i < m; ++i) t += x[i];
-      y += t;
+      const double* x = w.dc_of(tid / ntr) + static_cast<size_t>(t) * m;
+      double tt = x[m1];
+      for (int i = m1 + 1; i < m; ++i) tt += x[i];
+      y += tt;
     }
-    pot[tid] = y;
+    pot[(tid / ntr) * TMAX + t] = y;
   }
   __syncthreads();
 }
 
 // *out = blas_ddot_ones(cl, m), its 32 accumulator chains one per thread, the folds by thread 0
-__device__ void kpp_pot0(const WG& w, int m, double* part, double* out, int tid) {
+__device__ void kpp_pot0(const double* cl, int m, double* part, double* out, int tid) {
   const int n1 = m & -16, n32 = n1 & ~31;
-  if (tid < 32) part[tid] = chain_sum(w.cl, tid, n32, 32);  // Z[a][q] = chain of x[i + 8a + q]
+  if (tid < 32) part[tid] = chain_sum(cl, tid, n32, 32);  // Z[a][q] = chain of x[i + 8a + q]
   __syncthreads();
   if (tid == 0) {
     double A[4][4];
@@ -647,11 +758,11 @@ __device__ void kpp_pot0(const WG& w, int m, double* part, double* out, int tid)
       for (int q = 0; q < 4; ++q) A[a][q] = part[8 * a + q] + part[8 * a + q + 4];
     for (int i = n32; i < n1; i += 16)
       for (int a = 0; a < 4; ++a)
-        for (int q = 0; q < 4; ++q) A[a][q] += w.cl[i + 4 * a + q];
+        for (int q = 0; q < 4; ++q) A[a][q] += cl[i + 4 * a + q];
     double L[4];
     for (int q = 0; q < 4; ++q) L[q] = ((A[0][q] + A[1][q]) + A[2][q]) + A[3][q];
     double dot = (L[0] + L[2]) + (L[1] + L[3]);
-    for (int i = n1; i < m; ++i) dot += w.cl[i];
+    for (int i = n1; i < m; ++i) dot += cl[i];
     *out = dot;
   }
   __syncthreads();
@@ -666,12 +777,15 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   // arguments read from the workspace header (as in kmeans.hip): re-loaded where used rather
   // than pinned in SGPRs for the whole kernel
   const F64Args& a = *pa;
-  __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[TMAX], s_map[KMAX + 1];
-  __shared__ double s_pot[TMAX], s_tol, s_red[NT];
-  __shared__ int s_ired[NT];
-  __shared__ double s_stage[2 * CB];  // k-means++ search blocks / potential partials
-  __shared__ double s_thr[TMAX];
-  __shared__ int s_tix[TMAX];
+  __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[GMAX * TMAX], s_map[KMAX + 1];
+  __shared__ double s_pot[TMAX], s_tol;
+  __shared__ double s_stage[2 * CB > GMAX * 2 * CBM ? 2 * CB : GMAX * 2 * CBM];  // search blocks / potential partials
+  __shared__ double s_potg[GMAX];
+  __shared__ double s_cn[GMAX][KMAX + 1], s_sh[GMAX][KMAX + 1];  // per init: |c|^2, shift^2
+  __shared__ int s_cnt[GMAX][KMAX + 1];                          // per init: cluster counts
+  __shared__ int s_gof[GMAX];                                    // packed E-step: slot -> init
+  __shared__ double s_thrg[GMAX * TMAX], s_potm[GMAX * TMAX];   // k-means++ of the group
+  __shared__ int s_tixg[GMAX * TMAX], s_sflag[GMAX];
   const int tid = threadIdx.x;
   char* base = a.ws + static_cast<size_t>(blockIdx.x) * a.per_wg;
   WG w;
@@ -689,6 +803,9 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   w.xf = reinterpret_cast<double*>(base + a.o_xf);
   w.cf = reinterpret_cast<double*>(base + a.o_cf);
   const int m = a.m, d = a.d;
+  w.m = m;
+  w.kd = a.kd;
+  w.cfs = a.cfs;
 #ifdef CC_F64_STAMPS
   // the accumulators in LDS (thread 0's registers would move the kernel's allocation)
   __shared__ unsigned long long st_acc[11];
@@ -704,7 +821,10 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
     const int unit = s_unit;
     if (unit >= a.nh * a.nK) break;
     F64_STAMP(7);
-    const int hb = unit / a.nK, kk = unit - hb * a.nK;
+    // units in decreasing K, every resample's unit of the largest K first: the longest units
+    // start first and the short ones fill the tail (longest-processing-time order)
+    const int ki = unit / a.nh, hb = unit - ki * a.nh;
+    const int kk = a.korder[ki];
     const int h = a.h_begin + hb;
     const int K = a.Ks[kk];
     const int ntr = 2 + static_cast<int>(log(static_cast<double>(K)));
@@ -764,7 +884,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
     __syncthreads();
     // squared row norms of the centred rows
     for (int r = tid; r < m; r += NT) {
-      const double* x = xrow(w, d, r);
+      const XfRow x(w, d, r);
       w.xsq[r] = einsum_sq([&](int k) { return x[k]; }, d);
     }
     __syncthreads();
@@ -773,235 +893,302 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
 
     double best_inertia = 0.0;
     int best_iter = 0;
-    for (int init = 0; init < a.n_init; ++init) {
-      const double* u = a.kpp_u + (static_cast<size_t>(kk) * a.n_init + init) * a.kpp_stride + 1;
+    // the inits in lockstep groups of up to GMAX (in init order): every pass over the rows (the
+    // k-means++ distances, the E-step, the centre sums) serves all of the group's running inits;
+    // each init's values and their order are those of a run on its own
+    for (int g0 = 0; g0 < a.n_init; g0 += GMAX) {
+      const int G = a.n_init - g0 < GMAX ? a.n_init - g0 : GMAX;
       // ---- k-means++ -------------------------------------------------------------
-      int cpos = a.kpp_pos[kk * a.n_init + init];
-      for (int k = tid; k < d; k += NT) w.cen[k] = xrow(w, d, cpos)[k];
-      if (tid == 0) s_cand[0] = cpos;
+      int cpos[GMAX];
+      double pot[GMAX];
+#pragma unroll
+      for (int g = 0; g < GMAX; ++g) {
+        cpos[g] = g < G ? a.kpp_pos[kk * a.n_init + g0 + g] : 0;
+        pot[g] = 0.0;
+      }
+      for (int g = 0; g < G; ++g) {
+        double* cen = w.cen_of(g, 0);
+        for (int k = tid; k < d; k += NT) cen[k] = xrow(w, d, cpos[g])[k];
+        if (tid == 0) s_cand[g * TMAX] = cpos[g];
+      }
       __syncthreads();
-      kpp_mfma(w, d, m, s_cand, 1, true, tid);
-      kpp_pot0(w, m, s_stage, &s_pot[0], tid);
-      double pot = s_pot[0];
+      kpp_mfma_multi(w, d, m, s_cand, 1, G, true, tid);
+      for (int g = 0; g < G; ++g) {
+        kpp_pot0(w.cl_of(g), m, s_stage, &s_pot[0], tid);
+        pot[g] = s_pot[0];
+      }
       for (int c = 1; c < K; ++c) {
         // candidates: searchsorted(cumsum(closest), u * pot), clipped to m - 1
-        kpp_search(w, m, u + (c - 1) * ntr, pot, ntr, s_cand, s_stage, &s_flag, s_thr, s_tix, tid);
-        kpp_mfma(w, d, m, s_cand, ntr, false, tid);
-        kpp_pots(w, m, ntr, s_stage, s_pot, tid);
-        int bt = 0;
-        for (int t = 1; t < ntr; ++t)
-          if (s_pot[t] < s_pot[bt]) bt = t;
-        pot = s_pot[bt];
-        cpos = s_cand[bt];
-        for (int r = tid; r < m; r += NT) w.cl[r] = w.dc[static_cast<size_t>(bt) * m + r];
-        for (int k = tid; k < d; k += NT) w.cen[static_cast<size_t>(c) * d + k] = xrow(w, d, cpos)[k];
-        __syncthreads();
+        const double* uc[GMAX];
+#pragma unroll
+        for (int g = 0; g < GMAX; ++g)
+          uc[g] = a.kpp_u + (static_cast<size_t>(kk) * a.n_init + g0 + (g < G ? g : 0)) * a.kpp_stride + 1 +
+                  static_cast<size_t>(c - 1) * ntr;
+        kpp_search_multi(w, G, m, uc, pot, ntr, s_cand, s_stage, s_sflag, s_thrg, s_tixg, tid);
+        kpp_mfma_multi(w, d, m, s_cand, ntr, G, false, tid);
+        kpp_pots_multi(w, G, m, ntr, s_stage, s_potm, tid);
+        for (int g = 0; g < G; ++g) {
+          const double* sp = s_potm + g * TMAX;
+          int bt = 0;
+          for (int t = 1; t < ntr; ++t)
+            if (sp[t] < sp[bt]) bt = t;
+          pot[g] = sp[bt];
+          cpos[g] = s_cand[g * TMAX + bt];
+          double* cl = w.cl_of(g);
+          const double* dcb = w.dc_of(g) + static_cast<size_t>(bt) * m;
+          for (int r = tid; r < m; r += NT) cl[r] = dcb[r];
+          double* cen = w.cen_of(g, 0);
+          for (int k = tid; k < d; k += NT) cen[static_cast<size_t>(c) * d + k] = xrow(w, d, cpos[g])[k];
+          __syncthreads();
+        }
       }
       F64_STAMP(1);
       // ---- Lloyd -------------------------------------------------------------------
-      for (int r = tid; r < m; r += NT) w.lold[r] = -1;
-      bool strict = false;
-      int it = 0;
-      double* cen = w.cen;
-      double* cnew = w.cnew;
-      for (it = 0; it < a.max_iter; ++it) {
-        // |c|^2 into s_red[0..K)
+      for (int g = 0; g < G; ++g) {
+        int32_t* lold = w.lold_of(g);
+        for (int r = tid; r < m; r += NT) lold[r] = -1;
+      }
+      unsigned act = (1u << G) - 1u;  // running inits
+      unsigned par = 0;                // bit g: init g's current centres are in cnew
+      unsigned strict = 0;
+      int nit[GMAX];
+#pragma unroll
+      for (int g = 0; g < GMAX; ++g) nit[g] = a.max_iter;
+      for (int it = 0; it < a.max_iter && act; ++it) {
+        // |c|^2 into s_cn[g][0..K), the counts to zero
         __syncthreads();
-        for (int j = tid; j < K; j += NT) {
-          const double* cj = cen + static_cast<size_t>(j) * d;
-          s_red[j] = einsum_sq([&](int k) { return cj[k]; }, d);
+        for (int e = tid; e < G * K; e += NT) {
+          const int g = e / K, j = e - g * K;
+          s_cnt[g][j] = 0;
+          if (!((act >> g) & 1u)) continue;
+          const double* cj = w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(j) * d;
+          s_cn[g][j] = einsum_sq([&](int k) { return cj[k]; }, d);
         }
         __syncthreads();
-        int chg = 0;
-        for (int j = tid; j < K; j += NT) s_ired[j] = 0;
-        __syncthreads();
-        estep_mfma(w, cen, s_red, K, d, m, tid);
+        estep_multi(w, act, par, G, &s_cn[0][0], K, d, m, s_gof, tid);
         F64_STAMP(2);
 #ifdef CC_F64_STAMPS
         if (tid == 0) st_acc[8] += 1;
 #endif
-        for (int r = tid; r < m; r += NT) {
-          const int lab = w.lab[r];
-          chg |= (lab != w.lold[r]);
-          atomicAdd(&s_ired[lab], 1);  // counts (integers: order-free)
+        unsigned chg = 0;
+        for (int g = 0; g < G; ++g) {
+          if (!((act >> g) & 1u)) continue;
+          const int32_t* lab = w.lab_of(g);
+          const int32_t* lold = w.lold_of(g);
+          int c1 = 0;
+          for (int r = tid; r < m; r += NT) {
+            const int lb = lab[r];
+            c1 |= (lb != lold[r]);
+            atomicAdd(&s_cnt[g][lb], 1);  // counts (integers: order-free)
+          }
+          if (__syncthreads_or(c1)) chg |= 1u << g;
         }
-        const int changed = __syncthreads_or(chg);
         F64_STAMP(3);
-        msum_mfma(w, cnew, K, d, m, tid);
+        {
+          int na = 0;
+          for (int g = 0; g < G; ++g) na += (act >> g) & 1u;
+          msum_multi(w, par, na, s_gof, K, d, m, tid);
+        }
         F64_STAMP(4);
-        if (tid == 0) {
-          int ne = 0;
-          for (int j = 0; j < K; ++j) ne += (s_ired[j] == 0);
-          s_flag = ne;
+        for (int g = 0; g < G; ++g) {
+          if (!((act >> g) & 1u)) continue;
+          const double* cen = w.cen_of(g, (par >> g) & 1u);
+          double* cnew = w.cen_of(g, ((par >> g) & 1u) ^ 1u);
+          const int32_t* lab = w.lab_of(g);
+          int* cnt = s_cnt[g];
+          if (tid == 0) {
+            int ne = 0;
+            for (int j = 0; j < K; ++j) ne += (cnt[j] == 0);
+            s_flag = ne;
+          }
+          __syncthreads();
+          if (s_flag > 0) {
+            // _relocate_empty_clusters_dense: the empty clusters are fixed first (np.where), then
+            // each takes the farthest remaining row from its old centre (lowest index on ties)
+            for (int r = tid; r < m; r += NT) {
+              // ((X - centers_old[labels]) ** 2).sum(axis=1): numpy pairwise over the features
+              // (exact for d <= 128: one 8-accumulator block)
+              const double* c = cen + static_cast<size_t>(lab[r]) * d;
+              double sacc = 0.0;
+              if (d < 8) {
+                for (int k = 0; k < d; ++k) {
+                  const double e = xrow(w, d, r)[k] - c[k];
+                  sacc += e * e;
+                }
+              } else {
+                double v[8];
+                for (int q = 0; q < 8; ++q) {
+                  const double e = xrow(w, d, r)[q] - c[q];
+                  v[q] = e * e;
+                }
+                int k = 8;
+                for (; k < d - (d % 8); k += 8)
+                  for (int q = 0; q < 8; ++q) {
+                    const double e = xrow(w, d, r)[k + q] - c[k + q];
+                    v[q] += e * e;
+                  }
+                sacc = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+                for (; k < d; ++k) {
+                  const double e = xrow(w, d, r)[k] - c[k];
+                  sacc += e * e;
+                }
+              }
+              w.sq[r] = sacc;
+            }
+            __syncthreads();
+            if (tid == 0) {
+              double mx = 0.0;
+              for (int r = 0; r < m; ++r) mx = w.sq[r] > mx ? w.sq[r] : mx;
+              int ne = 0;
+              for (int j = 0; j < K; ++j)
+                if (cnt[j] == 0) s_map[ne++] = j;
+              s_flag = (mx == 0.0) ? 0 : ne;
+            }
+            __syncthreads();
+            // Parity gap (documented): sklearn takes the n_empty farthest rows from
+            // np.argpartition(distances, -n_empty)[:-n_empty-1:-1], whose order among those rows
+            // (and whose tie-break) is introselect's; here empty cluster e takes the e-th farthest
+            // remaining row, lowest index on ties.  The two agree for one empty cluster without
+            // tied distances; with n_empty >= 2 or ties, bit-parity with sklearn is not claimed.
+            const int ne = s_flag;
+            for (int e = 0; e < ne; ++e) {
+              if (tid == 0) {
+                int far = 0;
+                for (int r = 1; r < m; ++r)
+                  if (w.sq[r] > w.sq[far]) far = r;
+                s_best[0] = far;
+              }
+              __syncthreads();
+              const int far = s_best[0], j = s_map[e], old = lab[far];
+              for (int k = tid; k < d; k += NT) {
+                const double x = xrow(w, d, far)[k];
+                cnew[static_cast<size_t>(old) * d + k] -= x;
+                cnew[static_cast<size_t>(j) * d + k] = x;
+              }
+              __syncthreads();
+              if (tid == 0) {
+                cnt[j] = 1;
+                cnt[old] -= 1;
+                w.sq[far] = -1.0;
+              }
+              __syncthreads();
+            }
+          }
+          // _average_centers: in cluster order; an empty cluster copies argmax(weight)'s row as it
+          // stands (still a raw sum when the argmax comes later)
+          if (tid == 0) {
+            int am = 0;
+            for (int j = 1; j < K; ++j)
+              if (cnt[j] > cnt[am]) am = j;
+            s_best[1] = am;
+          }
+          __syncthreads();
+          const int am = s_best[1];
+          for (int k = tid; k < d; k += NT)
+            for (int j = 0; j < K; ++j) {
+              double* cj = cnew + static_cast<size_t>(j) * d;
+              if (cnt[j] > 0) cj[k] *= 1.0 / static_cast<double>(cnt[j]);
+              else cj[k] = cnew[static_cast<size_t>(am) * d + k];
+            }
+          __syncthreads();
+          // shifts and convergence
+          if (tid < K) {
+            const double sh = sqrt(euclid4(cnew + static_cast<size_t>(tid) * d, cen + static_cast<size_t>(tid) * d, d));
+            s_sh[g][tid] = sh * sh;
+          }
+          __syncthreads();
+        }
+        F64_STAMP(5);
+        for (int g = 0; g < G; ++g) {
+          if (!((act >> g) & 1u)) continue;
+          par ^= 1u << g;  // the new centres are current
+          if (!((chg >> g) & 1u)) {
+            strict |= 1u << g;
+            act &= ~(1u << g);
+            nit[g] = it + 1;
+            continue;
+          }
+          const double tot = np_pairwise(s_sh[g], K);
+          const int32_t* lab = w.lab_of(g);
+          int32_t* lold = w.lold_of(g);
+          for (int r = tid; r < m; r += NT) lold[r] = lab[r];
+          if (tot <= tol) {
+            act &= ~(1u << g);
+            nit[g] = it + 1;
+          }
+        }
+      }
+      __syncthreads();
+      const unsigned fin = ((1u << G) - 1u) & ~strict;  // final E-step against the last centres
+      if (fin) {
+        for (int e = tid; e < G * K; e += NT) {
+          const int g = e / K, j = e - g * K;
+          if (!((fin >> g) & 1u)) continue;
+          const double* cj = w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(j) * d;
+          s_cn[g][j] = einsum_sq([&](int k) { return cj[k]; }, d);
         }
         __syncthreads();
-        if (s_flag > 0) {
-          // _relocate_empty_clusters_dense: the empty clusters are fixed first (np.where), then
-          // each takes the farthest remaining row from its old centre (lowest index on ties)
-          for (int r = tid; r < m; r += NT) {
-            // ((X - centers_old[labels]) ** 2).sum(axis=1): numpy pairwise over the features
-            // (exact for d <= 128: one 8-accumulator block)
-            const double* c = cen + static_cast<size_t>(w.lab[r]) * d;
-            double s = 0.0;
-            if (d < 8) {
-              for (int k = 0; k < d; ++k) {
-                const double e = xrow(w, d, r)[k] - c[k];
-                s += e * e;
-              }
-            } else {
-              double v[8];
-              for (int q = 0; q < 8; ++q) {
-                const double e = xrow(w, d, r)[q] - c[q];
-                v[q] = e * e;
-              }
-              int k = 8;
-              for (; k < d - (d % 8); k += 8)
-                for (int q = 0; q < 8; ++q) {
-                  const double e = xrow(w, d, r)[k + q] - c[k + q];
-                  v[q] += e * e;
-                }
-              s = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-              for (; k < d; ++k) {
-                const double e = xrow(w, d, r)[k] - c[k];
-                s += e * e;
-              }
-            }
-            w.sq[r] = s;
+        estep_multi(w, fin, par, G, &s_cn[0][0], K, d, m, s_gof, tid);
+      }
+      // inertia of every init of the group in one pass over the rows: per-row squared distance to
+      // its centre (into the init's free k-means++ buffer), then each init's row-order sum on the
+      // first thread of its own wave
+      for (int r = tid; r < m; r += NT) {
+        const XfRow x(w, d, r);
+        for (int g = 0; g < G; ++g) {
+          const double* c = w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(w.lab_of(g)[r]) * d;
+          double res = 0.0;
+          const int n4 = d / 4, rem = d % 4;
+          for (int i = 0; i < n4; ++i) {
+            const double d0 = x[4 * i] - c[4 * i];
+            const double d1 = x[4 * i + 1] - c[4 * i + 1];
+            const double d2 = x[4 * i + 2] - c[4 * i + 2];
+            const double d3 = x[4 * i + 3] - c[4 * i + 3];
+            res += ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;
           }
+          for (int i = 0; i < rem; ++i) {
+            const double t = x[4 * n4 + i] - c[4 * n4 + i];
+            res += t * t;
+          }
+          w.dc_of(g)[r] = res;
+        }
+      }
+      __syncthreads();
+      if ((tid & 63) == 0 && (tid >> 6) < G) {
+        const double* sq = w.dc_of(tid >> 6);
+        double sacc = 0.0;
+        for (int r = 0; r < m; ++r) sacc += sq[r];
+        s_potg[tid >> 6] = sacc;
+      }
+      __syncthreads();
+      for (int g = 0; g < G; ++g) {
+        const int32_t* lab = w.lab_of(g);
+        const double inertia = s_potg[g];
+        const int n_iter = nit[g];
+        // best of n_init: lower inertia AND a different clustering
+        bool take = (g0 + g == 0);
+        if (!take && inertia < best_inertia) {
+          for (int j = tid; j <= KMAX; j += NT) s_map[j] = -1;
           __syncthreads();
           if (tid == 0) {
-            double mx = 0.0;
-            for (int r = 0; r < m; ++r) mx = w.sq[r] > mx ? w.sq[r] : mx;
-            int ne = 0;
-            for (int j = 0; j < K; ++j)
-              if (s_ired[j] == 0) s_map[ne++] = j;
-            s_flag = (mx == 0.0) ? 0 : ne;
+            int same = 1;
+            for (int r = 0; r < m && same; ++r) {
+              const int l1 = lab[r], l2 = w.lbest[r];
+              if (s_map[l1] == -1) s_map[l1] = l2;
+              else if (s_map[l1] != l2) same = 0;
+            }
+            s_flag = same;
           }
           __syncthreads();
-          // Parity gap (documented): sklearn takes the n_empty farthest rows from
-          // np.argpartition(distances, -n_empty)[:-n_empty-1:-1], whose order among those rows
-          // (and whose tie-break) is introselect's; here empty cluster e takes the e-th farthest
-          // remaining row, lowest index on ties.  The two agree for one empty cluster without
-          // tied distances; with n_empty >= 2 or ties, bit-parity with sklearn is not claimed.
-          const int ne = s_flag;
-          for (int e = 0; e < ne; ++e) {
-            if (tid == 0) {
-              int far = 0;
-              for (int r = 1; r < m; ++r)
-                if (w.sq[r] > w.sq[far]) far = r;
-              s_best[0] = far;
-            }
-            __syncthreads();
-            const int far = s_best[0], j = s_map[e], old = w.lab[far];
-            for (int k = tid; k < d; k += NT) {
-              const double x = xrow(w, d, far)[k];
-              cnew[static_cast<size_t>(old) * d + k] -= x;
-              cnew[static_cast<size_t>(j) * d + k] = x;
-            }
-            __syncthreads();
-            if (tid == 0) {
-              s_ired[j] = 1;
-              s_ired[old] -= 1;
-              w.sq[far] = -1.0;
-            }
-            __syncthreads();
-          }
+          take = !s_flag;
         }
-        // _average_centers: in cluster order; an empty cluster copies argmax(weight)'s row as it
-        // stands (still a raw sum when the argmax comes later)
-        if (tid == 0) {
-          int am = 0;
-          for (int j = 1; j < K; ++j)
-            if (s_ired[j] > s_ired[am]) am = j;
-          s_best[1] = am;
+        if (take) {
+          for (int r = tid; r < m; r += NT) w.lbest[r] = static_cast<uint8_t>(lab[r]);
+          best_inertia = inertia;
+          best_iter = n_iter;
         }
         __syncthreads();
-        const int am = s_best[1];
-        for (int k = tid; k < d; k += NT)
-          for (int j = 0; j < K; ++j) {
-            double* cj = cnew + static_cast<size_t>(j) * d;
-            if (s_ired[j] > 0) cj[k] *= 1.0 / static_cast<double>(s_ired[j]);
-            else cj[k] = cnew[static_cast<size_t>(am) * d + k];
-          }
-        __syncthreads();
-        // shifts and convergence
-        if (tid < K) {
-          const double sh = sqrt(euclid4(cnew + static_cast<size_t>(tid) * d, cen + static_cast<size_t>(tid) * d, d));
-          s_red[tid] = sh * sh;  // (the |c|^2 of this iteration are no longer read)
-        }
-        __syncthreads();
-        F64_STAMP(5);
-        double* tmp = cen;
-        cen = cnew;
-        cnew = tmp;
-        if (!changed) {
-          strict = true;
-          break;
-        }
-        const double tot = np_pairwise(s_red, K);
-        for (int r = tid; r < m; r += NT) w.lold[r] = w.lab[r];
-        if (tot <= tol) break;
       }
-      const int n_iter = (it < a.max_iter ? it : a.max_iter - 1) + 1;
-      __syncthreads();
-      if (!strict) {  // final E-step against the last centres
-        for (int j = tid; j < K; j += NT) {
-          const double* cj = cen + static_cast<size_t>(j) * d;
-          s_red[j] = einsum_sq([&](int k) { return cj[k]; }, d);
-        }
-        __syncthreads();
-        estep_mfma(w, cen, s_red, K, d, m, tid);
-      }
-      // inertia: per-row squared distance to its centre, summed in row order
-      for (int r = tid; r < m; r += NT) {
-        const double* c = cen + static_cast<size_t>(w.lab[r]) * d;
-        const double* x = xrow(w, d, r);
-        double res = 0.0;
-        const int n4 = d / 4, rem = d % 4;
-        for (int i = 0; i < n4; ++i) {
-          const double d0 = x[4 * i] - c[4 * i];
-          const double d1 = x[4 * i + 1] - c[4 * i + 1];
-          const double d2 = x[4 * i + 2] - c[4 * i + 2];
-          const double d3 = x[4 * i + 3] - c[4 * i + 3];
-          res += ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;
-        }
-        for (int i = 0; i < rem; ++i) {
-          const double t = x[4 * n4 + i] - c[4 * n4 + i];
-          res += t * t;
-        }
-        w.sq[r] = res;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        double s = 0.0;
-        for (int r = 0; r < m; ++r) s += w.sq[r];
-        s_pot[0] = s;
-      }
-      __syncthreads();
-      const double inertia = s_pot[0];
-      // best of n_init: lower inertia AND a different clustering
-      bool take = (init == 0);
-      if (!take && inertia < best_inertia) {
-        for (int j = tid; j <= KMAX; j += NT) s_map[j] = -1;
-        __syncthreads();
-        if (tid == 0) {
-          int same = 1;
-          for (int r = 0; r < m && same; ++r) {
-            const int l1 = w.lab[r], l2 = w.lbest[r];
-            if (s_map[l1] == -1) s_map[l1] = l2;
-            else if (s_map[l1] != l2) same = 0;
-          }
-          s_flag = same;
-        }
-        __syncthreads();
-        take = !s_flag;
-      }
-      if (take) {
-        for (int r = tid; r < m; r += NT) w.lbest[r] = static_cast<uint8_t>(w.lab[r]);
-        best_inertia = inertia;
-        best_iter = n_iter;
-      }
-      __syncthreads();
       F64_STAMP(6);
     }
     uint8_t* out = a.labels + static_cast<size_t>(kk) * a.n * a.ldl + h;
@@ -1021,6 +1208,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
 
 struct F64Layout {
   size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf, o_cf, per_wg;
+  size_t cfs;
 };
 
 F64Layout f64_layout(int m, int d, int kmax) {
@@ -1029,17 +1217,18 @@ F64Layout f64_layout(int m, int d, int kmax) {
   size_t o = 0;
   L.o_mean = o;  o += al(sizeof(double) * std::max(d, 1));
   L.o_xsq = o;   o += al(sizeof(double) * m);
-  L.o_cl = o;    o += al(sizeof(double) * m);
-  L.o_dc = o;    o += al(sizeof(double) * m * TMAX);
+  L.o_cl = o;    o += al(sizeof(double) * m * GMAX);
+  L.o_dc = o;    o += al(sizeof(double) * m * TMAX * GMAX);
   L.o_sq = o;    o += al(sizeof(double) * std::max(m, d));
-  L.o_cen = o;   o += al(sizeof(double) * kmax * d);
-  L.o_cnew = o;  o += al(sizeof(double) * kmax * d);
-  L.o_lab = o;   o += al(sizeof(int32_t) * m);
-  L.o_lold = o;  o += al(sizeof(int32_t) * m);
+  L.o_cen = o;   o += al(sizeof(double) * kmax * d * GMAX);
+  L.o_cnew = o;  o += al(sizeof(double) * kmax * d * GMAX);
+  L.o_lab = o;   o += al(sizeof(int32_t) * m * GMAX);
+  L.o_lold = o;  o += al(sizeof(int32_t) * m * GMAX);
   L.o_lbest = o; o += al(m);
   L.o_xc = o;    o += al(sizeof(double) * static_cast<size_t>(m) * d);
   L.o_xf = o;    o += al(sizeof(double) * static_cast<size_t>((m + 15) / 16) * 16 * ((d + 3) / 4) * 4);
-  L.o_cf = o;    o += al(sizeof(double) * static_cast<size_t>((kmax + 31) / 32) * 32 * ((d + 3) / 4) * 4);
+  L.cfs = static_cast<size_t>(std::max((kmax + 31) / 32, 1)) * 32 * ((d + 3) / 4) * 4;  // >= GMAX * TMAX rows
+  L.o_cf = o;    o += al(sizeof(double) * L.cfs * GMAX);
   L.per_wg = o;
   return L;
 }
@@ -1109,6 +1298,8 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.nh = nh;
   a.nK = nK;
   for (int i = 0; i < nK; ++i) a.Ks[i] = Ks[i];
+  for (int i = 0; i < nK; ++i) a.korder[i] = i;
+  std::stable_sort(a.korder, a.korder + nK, [&](int x, int y) { return Ks[x] > Ks[y]; });
   a.n_init = n_init;
   a.max_iter = max_iter;
   a.tol_rel = tol_rel;
@@ -1135,6 +1326,8 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.o_xc = L.o_xc;
   a.o_xf = L.o_xf;
   a.o_cf = L.o_cf;
+  a.kd = static_cast<size_t>(kmax) * d;
+  a.cfs = L.cfs;
   const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nK));
   // one upload: the zeroed counter and the arguments (a pageable source is consumed before
   // hipMemcpyAsync returns)
