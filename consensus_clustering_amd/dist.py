@@ -27,12 +27,23 @@ exchanged through a host copy; with ``nccl`` (RCCL) in place.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+# Diagnostics: run the exchange collectives even in a one-rank group (CCMI_DIST_EXCHANGE_W1=1), so
+# that a one-GPU box executes the RCCL calls of the N-GPU path (two ranks cannot share a device
+# under RCCL); the results are those of the skipped exchange.
+EXCHANGE_AT_W1 = os.environ.get("CCMI_DIST_EXCHANGE_W1") == "1"
 
 
 def _live() -> bool:
     return dist.is_available() and dist.is_initialized()
+
+
+def _exchange() -> bool:
+    return _live() and (dist.get_world_size() > 1 or EXCHANGE_AT_W1)
 
 
 def world() -> tuple:
@@ -56,7 +67,7 @@ def _host_staged(t: torch.Tensor) -> bool:
 
 
 def _all_reduce(t: torch.Tensor, op) -> torch.Tensor:
-    if not (_live() and dist.get_world_size() > 1):
+    if not _exchange():
         return t
     buf = t.cpu() if _host_staged(t) else t
     dist.all_reduce(buf, op=op)
@@ -92,7 +103,7 @@ def merge_labels(labels: torch.Tensor, H: int) -> torch.Tensor:
     labels: uint8 [nK, n, Hpad] (contiguous), this rank's columns ``shard(H, rank, W)`` filled
     (0xFF = not sampled).  After the call every rank holds every rank's columns.  Only the
     resample columns travel: a packed [nK, n, hw] block per rank, all-gathered."""
-    if not (_live() and dist.get_world_size() > 1):
+    if not _exchange():
         return labels
     rank, W = world()
     assert labels.is_contiguous() and labels.dtype == torch.uint8

@@ -3,7 +3,10 @@ as a W-rank torch.distributed job (gloo backend, every rank on cuda:0) and saves
 results.  It is started as a child process, so the ranks are spawned by a parent that has not
 touched the GPU.
 
-    python tests/dist_worker.py <fixture> <world> <keep 0|1> <out.npz>
+    python tests/dist_worker.py <fixture> <world> <keep 0|1> <out.npz> [backend]
+
+backend 'nccl' (RCCL) needs one device per rank, so on a one-GPU box it runs with world 1 and
+CCMI_DIST_EXCHANGE_W1=1 (the exchange collectives then run on RCCL anyway).
 """
 import os
 import socket
@@ -21,13 +24,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank(rank, world, port, name, keep, out):
+def _rank(rank, world, port, name, keep, out, backend="gloo"):
     import torch
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from consensus_clustering_amd import ConsensusClustering
         from tests.conftest import load_fixture
@@ -58,7 +64,8 @@ def main():
     import torch.multiprocessing as mp
 
     name, world, keep, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-    mp.spawn(_rank, args=(world, _free_port(), name, keep, out), nprocs=world, join=True)
+    backend = sys.argv[5] if len(sys.argv) > 5 else "gloo"
+    mp.spawn(_rank, args=(world, _free_port(), name, keep, out, backend), nprocs=world, join=True)
 
 
 if __name__ == "__main__":

@@ -44,3 +44,23 @@ def test_two_rank_fit_equals_one_rank(tmp_path, name, keep):
     if keep:
         np.testing.assert_array_equal(got["mij"], np.stack([cc.cdf_at_K_data[K]["mij"] for K in Ks]))
         np.testing.assert_array_equal(got["iij"], cc.cdf_at_K_data[Ks[0]]["iij"])
+
+
+@pytest.mark.parametrize("name,keep", [("blobs_n400_d8_k4", True), ("blobs_n150_d5_k3_h300", False)])
+def test_rccl_exchange_one_rank_equals_no_exchange(tmp_path, name, keep):
+    """The exchange collectives on RCCL (backend 'nccl'): one rank per device is all a one-GPU box
+    allows, so the fit runs in a one-rank RCCL group with the exchange forced on
+    (CCMI_DIST_EXCHANGE_W1=1: the label all-gather, the count and matrix SUM all-reduces) and must
+    equal the fit without any process group."""
+    out = str(tmp_path / "r0.npz")
+    env = dict(os.environ, PYTHONPATH=ROOT, CCMI_DIST_EXCHANGE_W1="1")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"), name, "1",
+                    str(int(keep)), out, "nccl"], check=True, timeout=300, env=env)
+    got = np.load(out)
+    cc = _one_rank(name, keep)
+    Ks = list(cc.cdf_at_K_data)
+    np.testing.assert_array_equal(got["pair_counts"], np.stack([cc.pair_counts_[K] for K in Ks]))
+    np.testing.assert_array_equal(got["labels"], cc.labels_.cpu().numpy())
+    np.testing.assert_array_equal(got["hist"], np.stack([cc.cdf_at_K_data[K]["hist"] for K in Ks]))
+    if keep:
+        np.testing.assert_array_equal(got["mij"], np.stack([cc.cdf_at_K_data[K]["mij"] for K in Ks]))
