@@ -18,6 +18,6 @@ cp $REPO/build/ccmi/*.o $W/build/ 2>/dev/null || true  # unchanged objects are r
 for o in kmeans $REBUILD; do rm -f $W/build/$o.o; done  # REBUILD="coassoc ...": objects whose flags change
 touch $W/build/*.o 2>/dev/null || true
 cd $W/consensus_clustering_amd/csrc
-make -j4 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $*" \
+make -j4 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -falign-loops=64 $*" \
   OUT=$REPO/consensus_clustering_amd/libccmi_$NAME.so BUILD=$W/build > $W/build.log 2>&1 || { tail -20 $W/build.log; exit 1; }
 echo built libccmi_$NAME.so
