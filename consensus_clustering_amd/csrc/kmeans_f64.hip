@@ -1155,9 +1155,19 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
       }
       __syncthreads();
       if ((tid & 63) == 0 && (tid >> 6) < G) {
+        // the row-order sum, its loads 16 rows ahead of the adds (one thread walking global
+        // memory otherwise waits a round trip per row)
         const double* sq = w.dc_of(tid >> 6);
         double sacc = 0.0;
-        for (int r = 0; r < m; ++r) sacc += sq[r];
+        int r = 0;
+        for (; r + 16 <= m; r += 16) {
+          double v[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) v[u] = sq[r + u];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) sacc += v[u];
+        }
+        for (; r < m; ++r) sacc += sq[r];
         s_potg[tid >> 6] = sacc;
       }
       __syncthreads();
@@ -1171,11 +1181,20 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
           for (int j = tid; j <= KMAX; j += NT) s_map[j] = -1;
           __syncthreads();
           if (tid == 0) {
+            // _is_same_clustering in row order, the labels loaded 16 rows ahead
             int same = 1;
-            for (int r = 0; r < m && same; ++r) {
-              const int l1 = lab[r], l2 = w.lbest[r];
-              if (s_map[l1] == -1) s_map[l1] = l2;
-              else if (s_map[l1] != l2) same = 0;
+            for (int r0 = 0; r0 < m && same; r0 += 16) {
+              int l1v[16], l2v[16];
+#pragma unroll
+              for (int u = 0; u < 16; ++u) {
+                l1v[u] = r0 + u < m ? lab[r0 + u] : 0;
+                l2v[u] = r0 + u < m ? static_cast<int>(w.lbest[r0 + u]) : 0;
+              }
+              for (int u = 0; u < 16 && r0 + u < m && same; ++u) {
+                const int l1 = l1v[u], l2 = l2v[u];
+                if (s_map[l1] == -1) s_map[l1] = l2;
+                else if (s_map[l1] != l2) same = 0;
+              }
             }
             s_flag = same;
           }
