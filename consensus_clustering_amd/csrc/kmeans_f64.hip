@@ -861,24 +861,43 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
     }
     __syncthreads();
     if (tid == 0) s_tol = (np_pairwise(w.sq, d) / d) * a.tol_rel;
-    // the centred rows, once per unit (the values every later step reads)
-    for (size_t e = tid; e < static_cast<size_t>(m) * d; e += NT) {
-      const int r = static_cast<int>(e / d), k = static_cast<int>(e - static_cast<size_t>(r) * d);
-      w.xc[e] = xc(a, idx, w.mean, r, k);
+    // the centred rows, once per unit (the values every later step reads): a thread keeps one
+    // feature and walks rows NT / d apart, four rows' gathers in flight (no 64-bit index division)
+    if (d <= NT) {
+      const int rpi = NT / d, rr = tid / d, kk = tid - (tid / d) * d;
+      if (rr < rpi) {
+        const double mu = w.mean[kk];
+        int r = rr;
+        for (; r + 3 * rpi < m; r += 4 * rpi) {
+          double v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = a.X[static_cast<size_t>(idx[r + u * rpi]) * d + kk];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) w.xc[static_cast<size_t>(r + u * rpi) * d + kk] = v[u] - mu;
+        }
+        for (; r < m; r += rpi) w.xc[static_cast<size_t>(r) * d + kk] = xc(a, idx, w.mean, r, kk);
+      }
+    } else {
+      for (int r = 0; r < m; ++r)
+        for (int k = tid; k < d; k += NT) w.xc[static_cast<size_t>(r) * d + k] = xc(a, idx, w.mean, r, k);
     }
     __syncthreads();
     // the same values as the matrix cores' B operand image: row tile t, k-step s, lane l holds
     // row 16t + (l & 15), feature 4s + (l >> 4) (exact zeros past m and d), so every operand
-    // load of a k-step is one contiguous 512-B piece
+    // load of a k-step is one contiguous 512-B piece; wave w writes the pieces (t, s) with
+    // t * S4 + s = w mod NT / 64
     {
       const int S4 = (d + 3) >> 2;
-      const size_t nf = static_cast<size_t>((m + 15) >> 4) * S4 * 64;
-      for (size_t e = tid; e < nf; e += NT) {
-        const int l = static_cast<int>(e & 63);
-        const size_t ts = e >> 6;
-        const int t = static_cast<int>(ts / S4), sk = static_cast<int>(ts - static_cast<size_t>(t) * S4);
-        const int r = 16 * t + (l & 15), k = 4 * sk + (l >> 4);
-        w.xf[e] = (r < m && k < d) ? w.xc[static_cast<size_t>(r) * d + k] : 0.0;
+      const int ntl = (m + 15) >> 4;
+      const int l = tid & 63, wv = tid >> 6;
+      const int rl = l & 15, kl = l >> 4;
+      for (int t = 0; t < ntl; ++t) {
+        const int r = 16 * t + rl;
+        for (int sk = (wv - t * S4 % (NT / 64) + (NT / 64)) % (NT / 64); sk < S4; sk += NT / 64) {
+          const int k = 4 * sk + kl;
+          w.xf[(static_cast<size_t>(t) * S4 + sk) * 64 + l] =
+              (r < m && k < d) ? w.xc[static_cast<size_t>(r) * d + k] : 0.0;
+        }
       }
     }
     __syncthreads();
