@@ -222,8 +222,8 @@ __device__ unsigned long long cc_f64_stamps[16];
   do {                                              \
     if (tid == 0) {                                 \
       const unsigned long long t_ = wall_clock64(); \
-      st_acc[ph] += t_ - st_acc[10];                \
-      st_acc[10] = t_;                              \
+      st_acc[ph] += t_ - st_acc[13];                \
+      st_acc[13] = t_;                              \
     }                                               \
   } while (0)
 #else
@@ -450,14 +450,15 @@ __device__ __forceinline__ void estep_multi(const WG& w, unsigned act, unsigned 
 // each value is kpp_mfma's ((-2 x.c) + |c|^2) + |x|^2 clipped at 0, min with init g's closest.
 __device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const int* cand, int ntr, int G, bool first,
                                                int tid) {
-  constexpr int RT = 2;
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int ntile = (m + 15) >> 4;
   const int nc = G * ntr;
   build_afrag(w.cf, [&](int j) { return w.xc + static_cast<size_t>(cand[(j / ntr) * TMAX + j % ntr]) * d; }, nc, d, tid);
   __syncthreads();
+  // one candidate tile: four row tiles per wave (four independent MFMA chains, more rows in flight)
   auto body = [&](auto ctc) __attribute__((always_inline)) {
     constexpr int CT = decltype(ctc)::value;
+    constexpr int RT = CT == 1 ? 4 : 2;
     const double* pa[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) pa[ct] = w.cf + static_cast<size_t>(ct) * ((d + 3) >> 2) * 64 + l;
@@ -808,10 +809,10 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   w.cfs = a.cfs;
 #ifdef CC_F64_STAMPS
   // the accumulators in LDS (thread 0's registers would move the kernel's allocation)
-  __shared__ unsigned long long st_acc[11];
+  __shared__ unsigned long long st_acc[14];
   if (tid == 0) {
-    for (int q = 0; q < 10; ++q) st_acc[q] = 0;
-    st_acc[10] = wall_clock64();
+    for (int q = 0; q < 13; ++q) st_acc[q] = 0;
+    st_acc[13] = wall_clock64();
   }
 #endif
   for (;;) {
@@ -943,9 +944,13 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
         for (int g = 0; g < GMAX; ++g)
           uc[g] = a.kpp_u + (static_cast<size_t>(kk) * a.n_init + g0 + (g < G ? g : 0)) * a.kpp_stride + 1 +
                   static_cast<size_t>(c - 1) * ntr;
+        F64_STAMP(1);
         kpp_search_multi(w, G, m, uc, pot, ntr, s_cand, s_stage, s_sflag, s_thrg, s_tixg, tid);
+        F64_STAMP(10);
         kpp_mfma_multi(w, d, m, s_cand, ntr, G, false, tid);
+        F64_STAMP(11);
         kpp_pots_multi(w, G, m, ntr, s_stage, s_potm, tid);
+        F64_STAMP(12);
         for (int g = 0; g < G; ++g) {
           const double* sp = s_potm + g * TMAX;
           int bt = 0;
@@ -1239,7 +1244,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
 #ifdef CC_F64_STAMPS
   if (tid == 0) {
     st_acc[9] = 1;
-    for (int q = 0; q < 10; ++q) atomicAdd(&cc_f64_stamps[q], st_acc[q]);
+    for (int q = 0; q < 13; ++q) atomicAdd(&cc_f64_stamps[q], st_acc[q]);
   }
 #endif
 }

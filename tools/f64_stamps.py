@@ -48,6 +48,8 @@ for i in range(0, len(args), 2):
     tot = float(out[:8].sum())
     print(f"{name} H={H} units={H * len(cfg['Ks'])} workgroups={int(out[9])}: {ms:.1f} ms; "
           f"Lloyd iterations {int(out[8])}")
-    for q in range(8):
-        print(f"  {NAMES[q]:16s} {100 * out[q] / tot:5.1f} %   {out[q] / 100e3 / max(int(out[9]), 1):9.1f} ms per workgroup")
+    tot += float(out[10:13].sum())
+    for q in list(range(8)) + [10, 11, 12]:
+        name = NAMES[q] if q < 8 else ["  k-means++ search", "  k-means++ distances", "  k-means++ potentials"][q - 10]
+        print(f"  {name:22s} {100 * out[q] / tot:5.1f} %   {out[q] / 100e3 / max(int(out[9]), 1):9.1f} ms per workgroup")
     sys.stdout.flush()
