@@ -40,6 +40,7 @@
 // per instruction; the rows enter as B operands from a fragment-ordered copy of the centred rows
 // (one contiguous 512-B load per k-step and row tile), the centres straight from their rows.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <cstring>
 
 #include <algorithm>
@@ -58,7 +59,12 @@ constexpr int NT = 256;
 constexpr int KMAX = 127;
 constexpr int TMAX = 6;
 constexpr int NKMAX = 64;
-constexpr int GMAX = 4;  // inits of a unit run in lockstep (groups of up to GMAX, in init order)
+// problems of a unit run in lockstep groups of up to GM (in unit order): the kernel is built for
+// GM = 4 (one K per unit, up to 4 inits) and GM = GMAX (two K's of 3 inits), see cc_kmeans_f64
+constexpr int GMAX = 6;
+constexpr int F64_KPACK = 2;        // K's per unit (at most GMAX / n_init)
+constexpr int F64_KPAIR_MAX = 127;  // only K's up to this are grouped
+constexpr int F64_UNITS_PER_WG = 4;  // ... and only with at least this many units per workgroup
 
 struct F64Args {
   const double* X;  // [n][d] (not centred)
@@ -68,6 +74,8 @@ struct F64Args {
   int nK;
   int Ks[NKMAX];
   int korder[NKMAX];  // K indices by decreasing K: units are dealt heaviest first
+  int ukfirst[NKMAX + 1];  // unit kind u: the K's korder[ukfirst[u] .. ukfirst[u + 1])
+  int nuk;
   int n_init, max_iter;
   double tol_rel;
   const double* kpp_u;  // [nK][n_init][stride]
@@ -354,28 +362,27 @@ __device__ __forceinline__ void build_afrag(double* dst, Row row, int nrow, int 
 // The E-step argmin of every row over the K centres: |c_j|^2 - 2 x.c_j (one rounding, as
 // sklearn's dgemm with beta = 1 on the centre norms), strict < over increasing j (a (value, index)
 // lexicographic minimum: lowest index on ties).  Each wave takes RT row tiles of 16 at a time.  The
-// running inits of the lockstep group share the pass: their centres are packed into one operand
-// image (slot a = the a-th running init, row J = a K + j; no per-init padding to 16 rows), each
-// pass of 16 CT rows feeds every init's own running (distance, label) per row (gof[a]: the init of
-// slot a; a = floor((J + 0.5) / K) in float32 is exact: J + 0.5 is at least 0.5 / K from an
-// integer), and a row tile's B operands are read once for all the inits.
-template <int RT, int CT>
-__device__ void estep_packed(const WG& w, int na, const int* gof, const double* cn, int K, int d, int m, int tid) {
+// running problems of the lockstep group (inits, and the K's of a multi-K unit) share the pass:
+// their centres are packed into one operand image (slot a = the a-th running problem, its K_a
+// centres at rows off_a .. off_a + K_a; no per-problem padding to 16 rows), each pass of 16 CT
+// rows feeds every problem's own running (distance, label) per row (jm[J] = a << 8 | j, gof[a]:
+// the problem of slot a), and a row tile's B operands are read once for all of them.
+template <int RT, int CT, int NA>
+__device__ void estep_packed(const WG& w, int na, const int* gof, const int* jm, const double* cnp, int nJ, int d,
+                             int m, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int ntile = (m + 15) >> 4;
-  const int nJ = na * K;
-  const float invK = 1.0f / static_cast<float>(K);
   for (int t0 = (tid >> 6) * RT; t0 < ntile; t0 += (NT / 64) * RT) {
     const double* pb[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
       pb[rt] = w.xf + static_cast<size_t>(t0 + rt < ntile ? t0 + rt : ntile - 1) * ((d + 3) >> 2) * 64 + l;
-    double bv[RT][GMAX];
-    int bj[RT][GMAX];
+    double bv[RT][NA];
+    int bj[RT][NA];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int a = 0; a < GMAX; ++a) {
+      for (int a = 0; a < NA; ++a) {
         bv[rt][a] = __builtin_inf();
         bj[rt][a] = 0x7fffffff;
       }
@@ -383,6 +390,9 @@ __device__ void estep_packed(const WG& w, int na, const int* gof, const double* 
       const double* pa[CT];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) pa[ct] = w.cf + static_cast<size_t>((J0 >> 4) + ct) * ((d + 3) >> 2) * 64 + l;
+      // the slots this tile of centres touches (wave-uniform: the others are skipped)
+      const int a0 = __builtin_amdgcn_readfirstlane(jm[J0] >> 8);
+      const int a1 = __builtin_amdgcn_readfirstlane(jm[(J0 + 16 * CT < nJ ? J0 + 16 * CT : nJ) - 1] >> 8);
       f64x4 acc[RT][CT];
       mfma_dots<RT, CT, 64, 64>(pa, pb, d, q, acc);
 #pragma unroll
@@ -391,20 +401,19 @@ __device__ void estep_packed(const WG& w, int na, const int* gof, const double* 
         for (int i = 0; i < 4; ++i) {
           const int J = J0 + 16 * ct + q + 4 * i;
           if (J >= nJ) continue;
-          const int a = static_cast<int>((static_cast<float>(J) + 0.5f) * invK);
-          const int j = J - a * K;
-          const double c2 = cn[gof[a] * (KMAX + 1) + j];
+          const int e = jm[J], a = e >> 8, j = e & 255;
+          const double c2 = cnp[J];
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) {
             const double v = __fma_rn(-2.0, acc[rt][ct][i], c2);
 #pragma unroll
-            for (int aa = 0; aa < GMAX; ++aa)
-              if (aa == a) lexmin(bv[rt][aa], bj[rt][aa], v, j);
+            for (int aa = 0; aa < NA; ++aa)
+              if (aa >= a0 && aa <= a1 && aa == a) lexmin(bv[rt][aa], bj[rt][aa], v, j);
           }
         }
     }
 #pragma unroll
-    for (int a = 0; a < GMAX; ++a) {
+    for (int a = 0; a < NA; ++a) {
       if (a >= na) break;
       int32_t* lab = w.lab_of(gof[a]);
 #pragma unroll
@@ -420,40 +429,73 @@ __device__ void estep_packed(const WG& w, int na, const int* gof, const double* 
   }
 }
 
-// par: bit g = which buffer holds init g's current centres (0: cen, 1: cnew)
-__device__ __forceinline__ void estep_multi(const WG& w, unsigned act, unsigned par, int G, const double* cn, int K,
-                                            int d, int m, int* gof, int tid) {
-  int na = 0;
+// The slot map of the running problems act (in problem order): gof[a] = the a-th running
+// problem, jm[J] = a << 8 | j for its centre j at packed row J, cnp[J] its |c|^2 (from cn, when
+// given).  Returns the number of rows; the maps are read after the caller's next barrier.
+__device__ __forceinline__ int slot_map(unsigned act, int G, const int* Kg, int* gof, int* jm, const double* cn,
+                                        double* cnp, int tid) {
+  int nJ = 0;
   for (int g = 0; g < G; ++g)
-    if ((act >> g) & 1u) {
-      if (tid == 0) gof[na] = g;
-      ++na;
-    }
-  // the running inits' centres, packed: row J = a K + j is centre j of the a-th running init
-  build_afrag(w.cf, [&](int J) {
-    int a = 0, g = 0;
-    for (; g < G; ++g)
+    if ((act >> g) & 1u) nJ += Kg[g];
+  for (int J = tid; J < nJ; J += NT) {
+    int a = 0, off = 0;
+    for (int g = 0; g < G; ++g)
       if ((act >> g) & 1u) {
-        if (a == J / K) break;
+        if (J < off + Kg[g]) {
+          jm[J] = (a << 8) | (J - off);
+          if (cn) cnp[J] = cn[g * (KMAX + 1) + J - off];
+          break;
+        }
+        off += Kg[g];
         ++a;
       }
-    return w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(J - (J / K) * K) * d;
-  }, na * K, d, tid);
-  __syncthreads();
-  if (na * K <= 16) estep_packed<2, 1>(w, na, gof, cn, K, d, m, tid);
-  else estep_packed<2, 2>(w, na, gof, cn, K, d, m, tid);
-  __syncthreads();
+  }
+  if (tid == 0) {
+    int a = 0;
+    for (int g = 0; g < G; ++g)
+      if ((act >> g) & 1u) gof[a++] = g;
+  }
+  return nJ;
 }
 
-// k-means++ distances of a lockstep group: init g's candidates are cand[g * TMAX + t], t < ntr
-// (first centre: ntr = 1), all G * ntr <= 24 of them as the centres of one pass over the rows;
-// each value is kpp_mfma's ((-2 x.c) + |c|^2) + |x|^2 clipped at 0, min with init g's closest.
-__device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const int* cand, int ntr, int G, bool first,
-                                               int tid) {
+// par: bit g = which buffer holds problem g's current centres (0: cen, 1: cnew)
+template <int GM>
+__device__ __forceinline__ int estep_multi(const WG& w, unsigned act, unsigned par, int G, const int* Kg,
+                                           const double* cn, double* cnp, int d, int m, int* gof, int* jm, int tid) {
+  const int nJ = slot_map(act, G, Kg, gof, jm, cn, cnp, tid);
+  __syncthreads();
+  int na = 0;
+  for (int g = 0; g < G; ++g) na += (act >> g) & 1u;
+  // the running problems' centres, packed
+  build_afrag(w.cf, [&](int J) {
+    const int e = jm[J], g = gof[e >> 8];
+    return w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(e & 255) * d;
+  }, nJ, d, tid);
+  __syncthreads();
+  // per-slot running minima for as many slots as run (registers: 3 * RT per slot)
+  if (GM > 4 && na <= GM / 2) {
+    if (nJ <= 16) estep_packed<2, 1, GM / 2>(w, na, gof, jm, cnp, nJ, d, m, tid);
+    else estep_packed<2, 2, GM / 2>(w, na, gof, jm, cnp, nJ, d, m, tid);
+  } else {
+    if (nJ <= 16) estep_packed<2, 1, GM>(w, na, gof, jm, cnp, nJ, d, m, tid);
+    else estep_packed<2, 2, GM>(w, na, gof, jm, cnp, nJ, d, m, tid);
+  }
+  __syncthreads();
+  return nJ;
+}
+
+// k-means++ distances of a lockstep group: column jj < nc is candidate t of problem g (col[jj] =
+// g << 8 | t, the candidate row cand[g * TMAX + t]; first centre: one column per problem), all
+// nc <= GMAX * TMAX of them as the centres of one pass over the rows; each value is kpp_mfma's
+// ((-2 x.c) + |c|^2) + |x|^2 clipped at 0, min with problem g's closest.
+__device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const int* cand, const int* col, int nc,
+                                               bool first, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int ntile = (m + 15) >> 4;
-  const int nc = G * ntr;
-  build_afrag(w.cf, [&](int j) { return w.xc + static_cast<size_t>(cand[(j / ntr) * TMAX + j % ntr]) * d; }, nc, d, tid);
+  build_afrag(w.cf, [&](int j) {
+    const int e = col[j];
+    return w.xc + static_cast<size_t>(cand[(e >> 8) * TMAX + (e & 255)]) * d;
+  }, nc, d, tid);
   __syncthreads();
   // one candidate tile: four row tiles per wave (four independent MFMA chains, more rows in flight)
   auto body = [&](auto ctc) __attribute__((always_inline)) {
@@ -479,7 +521,7 @@ __device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const 
           for (int i = 0; i < 4; ++i) {
             const int jj = 16 * ct + q + 4 * i;
             if (jj >= nc) continue;
-            const int g = jj / ntr, t = jj - g * ntr;
+            const int g = col[jj] >> 8, t = col[jj] & 255;
             double dd = -2.0 * acc[rt][ct][i];
             dd += w.xsq[cand[g * TMAX + t]];
             dd += w.xsq[r];
@@ -492,7 +534,8 @@ __device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const 
     }
   };
   if (nc <= 16) body(std::integral_constant<int, 1>{});
-  else body(std::integral_constant<int, 2>{});
+  else if (nc <= 32) body(std::integral_constant<int, 2>{});
+  else body(std::integral_constant<int, 3>{});
   __syncthreads();
 }
 
@@ -502,19 +545,17 @@ __device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const 
 // fma(1, x, acc) = acc + x is sklearn's addition (centers_new[j] += x * 1.0); fma(0, x, acc) =
 // acc + (+-0) = acc exactly for finite x, the accumulators starting at +0 and never -0 - so each
 // output is the row-order sum of its cluster's rows.  A wave owns CTP cluster tiles x FTP
-// 16-feature tiles per pass over the rows.  The running inits of the lockstep group share the pass:
-// their clusters are packed (slot a = the a-th running init, cluster row J = a K + j, so one tile
-// may hold clusters of two inits; lane l's A operand reads the labels of its own cluster's init),
-// and the B operands (the rows) are loaded once per k-step for all of them.
+// 16-feature tiles per pass over the rows.  The running problems of the lockstep group share the
+// pass: their clusters are packed as in the E-step (jm, gof: one tile may hold clusters of two
+// problems; lane l's A operand reads the labels of its own cluster's problem), and the B operands
+// (the rows) are loaded once per k-step for all of them.
 template <int CTP, int FTP>
-__device__ void msum_packed(const WG& w, unsigned par, int na, const int* gof, int K, int d, int m, int tid) {
+__device__ void msum_packed(const WG& w, unsigned par, const int* gof, const int* jm, int nJ, int d, int m, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
-  const int nJ = na * K;
   const int nct = (nJ + 15) >> 4, nft = (d + 15) >> 4;
   const int nfg = (nft + FTP - 1) / FTP;
   const int ncg = (nct + CTP - 1) / CTP;
   const int S = (m + 3) >> 2;
-  const float invK = 1.0f / static_cast<float>(K);
   for (int item = tid >> 6; item < ncg * nfg; item += NT / 64) {
     const int cg = item / nfg, fg = item - cg * nfg;
     int f[FTP];
@@ -530,9 +571,9 @@ __device__ void msum_packed(const WG& w, unsigned par, int na, const int* gof, i
 #pragma unroll
     for (int ct = 0; ct < CTP; ++ct) {
       const int J = (cg * CTP + ct) * 16 + c16;
-      const int a = J < nJ ? static_cast<int>((static_cast<float>(J) + 0.5f) * invK) : 0;
-      jl[ct] = J < nJ ? J - a * K : -2;
-      pl[ct] = w.lab_of(gof[a]) + q;
+      const int e = J < nJ ? jm[J] : 0;
+      jl[ct] = J < nJ ? (e & 255) : -2;
+      pl[ct] = w.lab_of(gof[e >> 8]) + q;
     }
     f64x4 acc[CTP][FTP];
 #pragma unroll
@@ -581,23 +622,22 @@ __device__ void msum_packed(const WG& w, unsigned par, int na, const int* gof, i
           for (int i = 0; i < 4; ++i) {
             const int J = (cg * CTP + ct) * 16 + q + 4 * i;
             if (J >= nJ) continue;
-            const int a = static_cast<int>((static_cast<float>(J) + 0.5f) * invK);
-            const int g = gof[a];
+            const int e = jm[J], g = gof[e >> 8];
             double* cnew = w.cen_of(g, ((par >> g) & 1u) ^ 1u);
-            cnew[static_cast<size_t>(J - a * K) * d + f[u]] = acc[ct][u][i];
+            cnew[static_cast<size_t>(e & 255) * d + f[u]] = acc[ct][u][i];
           }
   }
 }
 
-// the packed E-step's slot map must be current (estep_multi wrote gof for the same act)
-__device__ __forceinline__ void msum_multi(const WG& w, unsigned par, int na, const int* gof, int K, int d, int m,
-                                           int tid) {
-  const int nct = (na * K + 15) >> 4, nft = (d + 15) >> 4;
+// the packed E-step's slot map must be current (estep_multi wrote gof / jm for the same act)
+__device__ __forceinline__ void msum_multi(const WG& w, unsigned par, const int* gof, const int* jm, int nJ, int d,
+                                           int m, int tid) {
+  const int nct = (nJ + 15) >> 4, nft = (d + 15) >> 4;
   // as many cluster tiles per wave as keep every wave busy: each cluster-tile group re-reads the
   // rows, and the passes over the rows are what the sums wait on
-  if (nct >= 3 && ((nct + 3) / 4) * nft >= NT / 64) msum_packed<4, 1>(w, par, na, gof, K, d, m, tid);
-  else if (nct >= 2 && ((nct + 1) / 2) * nft >= NT / 64) msum_packed<2, 1>(w, par, na, gof, K, d, m, tid);
-  else msum_packed<1, 1>(w, par, na, gof, K, d, m, tid);
+  if (nct >= 3 && ((nct + 3) / 4) * nft >= NT / 64) msum_packed<4, 1>(w, par, gof, jm, nJ, d, m, tid);
+  else if (nct >= 2 && ((nct + 1) / 2) * nft >= NT / 64) msum_packed<2, 1>(w, par, gof, jm, nJ, d, m, tid);
+  else msum_packed<1, 1>(w, par, gof, jm, nJ, d, m, tid);
   __syncthreads();
 }
 
@@ -608,22 +648,38 @@ __device__ __forceinline__ void msum_multi(const WG& w, unsigned par, int na, co
 // workgroup (the BLAS potentials, whose accumulators are independent until their final folds).
 constexpr int CB = 1024;  // search staging block (doubles); the LDS area holds 2 * CB
 
-// kpp_search for every init of a lockstep group at once: init g's walk runs on the first thread
-// of wave g (the walks of different inits overlap), each over its own staged blocks of CBM values
-// (sb: [GMAX][2][CBM]).  Init g: cand[g TMAX + t] = searchsorted(cumsum(cl_g), u[g][t] pot[g])
-// clipped to m - 1, t < ntr: the float64 cumulative sum in row order, 8 partial sums then one
-// comparison with the next of the sorted thresholds (the sums do not decrease, so the
-// thresholds are crossed in order).
+// The group's per-problem facts, in LDS: K, candidates per step (2 + ln K), K index, init.
+struct GroupInfo {
+  const int *K, *ntr, *kk, *ini;
+};
+
+// the walker thread of slot s (< GMAX): lanes 0 and 32 of wave s mod 4
+__device__ __forceinline__ int walker_slot(int tid) {
+  return (tid & 31) == 0 ? (tid >> 6) + (NT / 64) * ((tid >> 5) & 1) : GMAX;
+}
+
+// kpp_search for every seeding problem of a lockstep group at once (slot s: problem sg[s], s <
+// ns): each walk runs on its own walker thread (the walks overlap), over its own staged blocks of
+// CBM values (sb: [GMAX][2][CBM]).  Problem g at step c: cand[g TMAX + t] =
+// searchsorted(cumsum(cl_g), u_g[c][t] pot[g]) clipped to m - 1, t < ntr_g: the float64
+// cumulative sum in row order, 8 partial sums then one comparison with the next of the sorted
+// thresholds (the sums do not decrease, so the thresholds are crossed in order).
 constexpr int CBM = 512;
-__device__ void kpp_search_multi(const WG& w, int G, int m, const double* const (&u)[GMAX], const double (&pot)[GMAX],
-                                 int ntr, int* cand, double* sb, int* sflag, double* s_thr, int* s_tix, int tid) {
-  const int wv = tid >> 6;
-  const bool walker = (tid & 63) == 0 && wv < G;
+__device__ void kpp_search_multi(const F64Args& a, const WG& w, const GroupInfo& gi, const int* sg, int ns, int c,
+                                 const double* pot, int* cand, double* sb, int* sflag, double* s_thr, int* s_tix,
+                                 int tid) {
+  const int m = w.m;
+  const int ws = walker_slot(tid);
+  const bool walker = ws < ns;
+  const int gw = walker ? sg[ws] : 0;
+  const int ntr = walker ? gi.ntr[gw] : 0;
   if (walker) {
-    double* thr = s_thr + wv * TMAX;
-    int* tix = s_tix + wv * TMAX;
+    const double* u = a.kpp_u + (static_cast<size_t>(gi.kk[gw]) * a.n_init + gi.ini[gw]) * a.kpp_stride + 1 +
+                      static_cast<size_t>(c - 1) * ntr;
+    double* thr = s_thr + ws * TMAX;
+    int* tix = s_tix + ws * TMAX;
     for (int t = 0; t < ntr; ++t) {
-      thr[t] = u[wv][t] * pot[wv];
+      thr[t] = u[t] * pot[gw];
       tix[t] = t;
     }
     for (int t = 1; t < ntr; ++t)  // insertion sort of the thresholds (ties: either order)
@@ -635,55 +691,55 @@ __device__ void kpp_search_multi(const WG& w, int G, int m, const double* const 
         tix[v] = tix[v - 1];
         tix[v - 1] = y;
       }
-    for (int t = 0; t < ntr; ++t) cand[wv * TMAX + t] = m - 1;  // not crossed: clipped to m - 1
-    sflag[wv] = 0;
+    for (int t = 0; t < ntr; ++t) cand[gw * TMAX + t] = m - 1;  // not crossed: clipped to m - 1
+    sflag[ws] = 0;
   }
-  for (int e = tid; e < G * CBM; e += NT) {
-    const int g = e / CBM, i = e - g * CBM;
-    if (i < m) sb[g * 2 * CBM + i] = w.cl_of(g)[i];
+  for (int e = tid; e < ns * CBM; e += NT) {
+    const int s = e / CBM, i = e - s * CBM;
+    if (i < m) sb[s * 2 * CBM + i] = w.cl_of(sg[s])[i];
   }
   __syncthreads();
-  double cum = 0.0, tn = walker ? s_thr[wv * TMAX] : 0.0;
+  double cum = 0.0, tn = walker ? s_thr[ws * TMAX] : 0.0;
   int next = 0;
   int buf = 0;
   for (int b0 = 0; b0 < m; b0 += CBM) {
     const int nb = b0 + CBM;
-    for (int e = tid; e < G * CBM; e += NT) {
-      const int g = e / CBM, i = e - g * CBM;
-      if (nb + i < m) sb[(g * 2 + (buf ^ 1)) * CBM + i] = w.cl_of(g)[nb + i];
+    for (int e = tid; e < ns * CBM; e += NT) {
+      const int s = e / CBM, i = e - s * CBM;
+      if (nb + i < m) sb[(s * 2 + (buf ^ 1)) * CBM + i] = w.cl_of(sg[s])[nb + i];
     }
-    if (walker && !sflag[wv]) {
-      const double* cur = sb + (wv * 2 + buf) * CBM;
-      const double* thr = s_thr + wv * TMAX;
-      const int* tix = s_tix + wv * TMAX;
+    if (walker && !sflag[ws]) {
+      const double* cur = sb + (ws * 2 + buf) * CBM;
+      const double* thr = s_thr + ws * TMAX;
+      const int* tix = s_tix + ws * TMAX;
       const int n = m - b0 < CBM ? m - b0 : CBM;
       for (int i0 = 0; i0 < n && next < ntr; i0 += 8) {
         // 8 partial sums, then one comparison with the next threshold (the sums do not decrease)
         double cs[8];
         const int g8 = n - i0 < 8 ? n - i0 : 8;
-        double c = cum;
+        double cc = cum;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          if (i < g8) c += cur[i0 + i];
-          cs[i] = c;
+          if (i < g8) cc += cur[i0 + i];
+          cs[i] = cc;
         }
-        if (!(c < tn)) {
+        if (!(cc < tn)) {
 #pragma unroll
           for (int i = 0; i < 8; ++i)
             while (i < g8 && next < ntr && !(cs[i] < tn)) {
               const int p = b0 + i0 + i;
-              cand[wv * TMAX + tix[next]] = p < m - 1 ? p : m - 1;
+              cand[gw * TMAX + tix[next]] = p < m - 1 ? p : m - 1;
               ++next;
               tn = next < ntr ? thr[next] : 0.0;
             }
         }
-        cum = c;
+        cum = cc;
       }
-      if (next >= ntr) sflag[wv] = 1;
+      if (next >= ntr) sflag[ws] = 1;
     }
     __syncthreads();
     int all = 1;
-    for (int g = 0; g < G; ++g) all &= sflag[g];
+    for (int q = 0; q < ns; ++q) all &= sflag[q];
     if (all) break;
     buf ^= 1;
   }
@@ -704,30 +760,34 @@ __device__ __forceinline__ double chain_sum(const double* x, int i0, int e, int 
   return acc;
 }
 
-// The candidates' potentials for every init of a lockstep group at once: pot[g TMAX + t] =
-// blas_gemv_t_ones(column (g, t) = w.dc_of(g) + t m, m, t, ntr), its (column, 2048-row block,
-// lane) accumulator chains one per thread, the folds by thread g ntr + t.
-__device__ void kpp_pots_multi(const WG& w, int G, int m, int ntr, double* part, double* pot, int tid) {
-  const int n4 = ntr & ~3, rem = ntr - n4;
+// The candidates' potentials for every column of a lockstep group at once (col[c] = g << 8 | t):
+// pot[g TMAX + t] = blas_gemv_t_ones(column t of w.dc_of(g), m, t, ntr_g), its (column,
+// 2048-row block, lane) accumulator chains one per thread, the folds by thread c.
+__device__ void kpp_pots_multi(const WG& w, const int* ntrg, const int* col, int nc, double* part, double* pot,
+                               int tid) {
+  const int m = w.m;
   const int m1 = m & ~3;
   const int nb = (m1 + 2047) / 2048;
-  const int nc = G * ntr;
   const int GB = (2 * CB) / (nc * 4);  // blocks per round
+  // the lane count of column c's 4-lane / 2-lane grouping
+  auto lanes = [&](int c) {
+    const int t = col[c] & 255, ntr = ntrg[col[c] >> 8];
+    const int n4 = ntr & ~3;
+    return (ntr - n4 >= 2 && t >= n4 && t < n4 + 2) ? 2 : 4;
+  };
   double y = 0.0;
   for (int bb = 0; bb < nb; bb += GB) {
     const int gb = nb - bb < GB ? nb - bb : GB;
     for (int ch = tid; ch < nc * gb * 4; ch += NT) {
       const int c = ch / (gb * 4), g = (ch >> 2) % gb, q = ch & 3;
-      const int t = c % ntr;
-      const int L = (rem >= 2 && t >= n4 && t < n4 + 2) ? 2 : 4;
+      const int L = lanes(c);
       if (q >= L) continue;
       const int b = (bb + g) * 2048, e = b + 2048 < m1 ? b + 2048 : m1;
-      part[(c * GB + g) * 4 + q] = chain_sum(w.dc_of(c / ntr) + static_cast<size_t>(t) * m, b + q, e, L);
+      part[(c * GB + g) * 4 + q] = chain_sum(w.dc_of(col[c] >> 8) + static_cast<size_t>(col[c] & 255) * m, b + q, e, L);
     }
     __syncthreads();
     if (tid < nc) {
-      const int t = tid % ntr;
-      const bool two = rem >= 2 && t >= n4 && t < n4 + 2;
+      const bool two = lanes(tid) == 2;
       for (int g = 0; g < gb; ++g) {
         const double* pp = part + (tid * GB + g) * 4;
         y += two ? pp[0] + pp[1] : (pp[0] + pp[2]) + (pp[1] + pp[3]);
@@ -736,14 +796,14 @@ __device__ void kpp_pots_multi(const WG& w, int G, int m, int ntr, double* part,
     __syncthreads();
   }
   if (tid < nc) {
-    const int t = tid % ntr;
+    const int g = col[tid] >> 8, t = col[tid] & 255;
     if (m1 < m) {
-      const double* x = w.dc_of(tid / ntr) + static_cast<size_t>(t) * m;
+      const double* x = w.dc_of(g) + static_cast<size_t>(t) * m;
       double tt = x[m1];
       for (int i = m1 + 1; i < m; ++i) tt += x[i];
       y += tt;
     }
-    pot[(tid / ntr) * TMAX + t] = y;
+    pot[g * TMAX + t] = y;
   }
   __syncthreads();
 }
@@ -774,19 +834,27 @@ __device__ __forceinline__ double xc(const F64Args& a, const int32_t* idx, const
   return a.X[static_cast<size_t>(idx[r]) * a.d + k] - mean[k];
 }
 
+template <int GM>
 __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __restrict__ pa) {
   // arguments read from the workspace header (as in kmeans.hip): re-loaded where used rather
   // than pinned in SGPRs for the whole kernel
   const F64Args& a = *pa;
-  __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[GMAX * TMAX], s_map[KMAX + 1];
-  __shared__ double s_pot[TMAX], s_tol;
-  __shared__ double s_stage[2 * CB > GMAX * 2 * CBM ? 2 * CB : GMAX * 2 * CBM];  // search blocks / potential partials
-  __shared__ double s_potg[GMAX];
-  __shared__ double s_cn[GMAX][KMAX + 1], s_sh[GMAX][KMAX + 1];  // per init: |c|^2, shift^2
-  __shared__ int s_cnt[GMAX][KMAX + 1];                          // per init: cluster counts
-  __shared__ int s_gof[GMAX];                                    // packed E-step: slot -> init
-  __shared__ double s_thrg[GMAX * TMAX], s_potm[GMAX * TMAX];   // k-means++ of the group
-  __shared__ int s_tixg[GMAX * TMAX], s_sflag[GMAX];
+  __shared__ int s_unit, s_flag, s_best[TMAX + 1], s_cand[GM * TMAX], s_map[KMAX + 1];
+  __shared__ double s_tol;
+  __shared__ double s_stage[2 * CB > GM * 2 * CBM ? 2 * CB : GM * 2 * CBM];  // search blocks / potential partials
+  __shared__ double s_potg[GM], s_potc[GM];
+  __shared__ double s_cn[GM][KMAX + 1], s_sh[GM][KMAX + 1];  // per problem: |c|^2, shift^2
+  __shared__ int s_cnt[GM][KMAX + 1];                          // per problem: cluster counts
+  __shared__ int s_gof[GM], s_jm[GM * KMAX];                 // packed E-step: slot / row maps
+  __shared__ double s_cnp[GM * KMAX];                          // packed E-step: |c|^2 by row
+  __shared__ double s_thrg[GM * TMAX], s_potm[GM * TMAX];   // k-means++ of the group
+  __shared__ int s_tixg[GM * TMAX], s_sflag[GM], s_col[GM * TMAX], s_sg[GM];
+  __shared__ int s_K[GM], s_ntr[GM], s_kk[GM], s_ini[GM];  // the group's problems
+  GroupInfo gi;
+  gi.K = s_K;
+  gi.ntr = s_ntr;
+  gi.kk = s_kk;
+  gi.ini = s_ini;
   const int tid = threadIdx.x;
   char* base = a.ws + static_cast<size_t>(blockIdx.x) * a.per_wg;
   WG w;
@@ -820,15 +888,14 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
     if (tid == 0) s_unit = static_cast<int>(atomicAdd(a.counter, 1u));
     __syncthreads();
     const int unit = s_unit;
-    if (unit >= a.nh * a.nK) break;
+    if (unit >= a.nh * a.nuk) break;
     F64_STAMP(7);
-    // units in decreasing K, every resample's unit of the largest K first: the longest units
-    // start first and the short ones fill the tail (longest-processing-time order)
-    const int ki = unit / a.nh, hb = unit - ki * a.nh;
-    const int kk = a.korder[ki];
+    // unit kinds in decreasing K, every resample's unit of the heaviest kind first: the longest
+    // units start first and the short ones fill the tail (longest-processing-time order).  A kind
+    // is one K or a run of adjacent K's (korder[kf .. kf + P)) whose problems share the passes.
+    const int ui = unit / a.nh, hb = unit - ui * a.nh;
+    const int kf = a.ukfirst[ui], nprob = (a.ukfirst[ui + 1] - kf) * a.n_init;
     const int h = a.h_begin + hb;
-    const int K = a.Ks[kk];
-    const int ntr = 2 + static_cast<int>(log(static_cast<double>(K)));
     const int32_t* idx = a.idx + static_cast<size_t>(h) * m;
 
     // column means (rows in order), then variances of the centred columns
@@ -913,58 +980,74 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
 
     double best_inertia = 0.0;
     int best_iter = 0;
-    // the inits in lockstep groups of up to GMAX (in init order): every pass over the rows (the
-    // k-means++ distances, the E-step, the centre sums) serves all of the group's running inits;
-    // each init's values and their order are those of a run on its own
-    for (int g0 = 0; g0 < a.n_init; g0 += GMAX) {
-      const int G = a.n_init - g0 < GMAX ? a.n_init - g0 : GMAX;
-      // ---- k-means++ -------------------------------------------------------------
-      int cpos[GMAX];
-      double pot[GMAX];
-#pragma unroll
-      for (int g = 0; g < GMAX; ++g) {
-        cpos[g] = g < G ? a.kpp_pos[kk * a.n_init + g0 + g] : 0;
-        pot[g] = 0.0;
-      }
-      for (int g = 0; g < G; ++g) {
-        double* cen = w.cen_of(g, 0);
-        for (int k = tid; k < d; k += NT) cen[k] = xrow(w, d, cpos[g])[k];
-        if (tid == 0) s_cand[g * TMAX] = cpos[g];
+    // the unit's problems (K-major: every init of its first K, then of the next) in lockstep
+    // groups of up to GM: every pass over the rows (the k-means++ distances, the E-step, the
+    // centre sums) serves all of the group's running problems; each problem's values and their
+    // order are those of a run on its own
+    for (int g0 = 0; g0 < nprob; g0 += GM) {
+      const int G = nprob - g0 < GM ? nprob - g0 : GM;
+      __syncthreads();
+      if (tid < G) {
+        const int e = g0 + tid, q = e / a.n_init;
+        const int kk = a.korder[kf + q];
+        s_kk[tid] = kk;
+        s_ini[tid] = e - q * a.n_init;
+        s_K[tid] = a.Ks[kk];
+        s_ntr[tid] = 2 + static_cast<int>(log(static_cast<double>(a.Ks[kk])));
       }
       __syncthreads();
-      kpp_mfma_multi(w, d, m, s_cand, 1, G, true, tid);
+      int KM = 0;
+      for (int g = 0; g < G; ++g) KM = s_K[g] > KM ? s_K[g] : KM;
+      // ---- k-means++ -------------------------------------------------------------
       for (int g = 0; g < G; ++g) {
-        kpp_pot0(w.cl_of(g), m, s_stage, &s_pot[0], tid);
-        pot[g] = s_pot[0];
+        const int cp = a.kpp_pos[s_kk[g] * a.n_init + s_ini[g]];
+        double* cen = w.cen_of(g, 0);
+        for (int k = tid; k < d; k += NT) cen[k] = xrow(w, d, cp)[k];
+        if (tid == 0) {
+          s_cand[g * TMAX] = cp;
+          s_col[g] = g << 8;
+        }
       }
-      for (int c = 1; c < K; ++c) {
+      __syncthreads();
+      kpp_mfma_multi(w, d, m, s_cand, s_col, G, true, tid);
+      for (int g = 0; g < G; ++g) {
+        kpp_pot0(w.cl_of(g), m, s_stage, &s_potc[g], tid);
+      }
+      for (int c = 1; c < KM; ++c) {
+        // the problems still seeding (c < K_g), their candidate columns
+        int ns = 0, nc = 0;
+        for (int g = 0; g < G; ++g)
+          if (c < s_K[g]) {
+            if (tid == 0) s_sg[ns] = g;
+            if (tid < s_ntr[g]) s_col[nc + tid] = (g << 8) | tid;
+            ++ns;
+            nc += s_ntr[g];
+          }
+        __syncthreads();
         // candidates: searchsorted(cumsum(closest), u * pot), clipped to m - 1
-        const double* uc[GMAX];
-#pragma unroll
-        for (int g = 0; g < GMAX; ++g)
-          uc[g] = a.kpp_u + (static_cast<size_t>(kk) * a.n_init + g0 + (g < G ? g : 0)) * a.kpp_stride + 1 +
-                  static_cast<size_t>(c - 1) * ntr;
         F64_STAMP(1);
-        kpp_search_multi(w, G, m, uc, pot, ntr, s_cand, s_stage, s_sflag, s_thrg, s_tixg, tid);
+        kpp_search_multi(a, w, gi, s_sg, ns, c, s_potc, s_cand, s_stage, s_sflag, s_thrg, s_tixg, tid);
         F64_STAMP(10);
-        kpp_mfma_multi(w, d, m, s_cand, ntr, G, false, tid);
+        kpp_mfma_multi(w, d, m, s_cand, s_col, nc, false, tid);
         F64_STAMP(11);
-        kpp_pots_multi(w, G, m, ntr, s_stage, s_potm, tid);
+        kpp_pots_multi(w, s_ntr, s_col, nc, s_stage, s_potm, tid);
         F64_STAMP(12);
-        for (int g = 0; g < G; ++g) {
+        for (int q = 0; q < ns; ++q) {
+          const int g = s_sg[q];
           const double* sp = s_potm + g * TMAX;
           int bt = 0;
-          for (int t = 1; t < ntr; ++t)
+          for (int t = 1; t < s_ntr[g]; ++t)
             if (sp[t] < sp[bt]) bt = t;
-          pot[g] = sp[bt];
-          cpos[g] = s_cand[g * TMAX + bt];
+          const int cp = s_cand[g * TMAX + bt];
           double* cl = w.cl_of(g);
           const double* dcb = w.dc_of(g) + static_cast<size_t>(bt) * m;
           for (int r = tid; r < m; r += NT) cl[r] = dcb[r];
           double* cen = w.cen_of(g, 0);
-          for (int k = tid; k < d; k += NT) cen[static_cast<size_t>(c) * d + k] = xrow(w, d, cpos[g])[k];
+          for (int k = tid; k < d; k += NT) cen[static_cast<size_t>(c) * d + k] = xrow(w, d, cp)[k];
           __syncthreads();
+          if (tid == 0) s_potc[g] = sp[bt];
         }
+        __syncthreads();
       }
       F64_STAMP(1);
       // ---- Lloyd -------------------------------------------------------------------
@@ -972,24 +1055,24 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
         int32_t* lold = w.lold_of(g);
         for (int r = tid; r < m; r += NT) lold[r] = -1;
       }
-      unsigned act = (1u << G) - 1u;  // running inits
-      unsigned par = 0;                // bit g: init g's current centres are in cnew
+      unsigned act = (1u << G) - 1u;  // running problems
+      unsigned par = 0;                // bit g: problem g's current centres are in cnew
       unsigned strict = 0;
-      int nit[GMAX];
+      int nit[GM];
 #pragma unroll
-      for (int g = 0; g < GMAX; ++g) nit[g] = a.max_iter;
+      for (int g = 0; g < GM; ++g) nit[g] = a.max_iter;
       for (int it = 0; it < a.max_iter && act; ++it) {
-        // |c|^2 into s_cn[g][0..K), the counts to zero
+        // |c|^2 into s_cn[g][0..K_g), the counts to zero
         __syncthreads();
-        for (int e = tid; e < G * K; e += NT) {
-          const int g = e / K, j = e - g * K;
-          s_cnt[g][j] = 0;
-          if (!((act >> g) & 1u)) continue;
-          const double* cj = w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(j) * d;
-          s_cn[g][j] = einsum_sq([&](int k) { return cj[k]; }, d);
-        }
+        for (int g = 0; g < G; ++g)
+          for (int j = tid; j < s_K[g]; j += NT) {
+            s_cnt[g][j] = 0;
+            if (!((act >> g) & 1u)) continue;
+            const double* cj = w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(j) * d;
+            s_cn[g][j] = einsum_sq([&](int k) { return cj[k]; }, d);
+          }
         __syncthreads();
-        estep_multi(w, act, par, G, &s_cn[0][0], K, d, m, s_gof, tid);
+        const int nJ = estep_multi<GM>(w, act, par, G, s_K, &s_cn[0][0], s_cnp, d, m, s_gof, s_jm, tid);
         F64_STAMP(2);
 #ifdef CC_F64_STAMPS
         if (tid == 0) st_acc[8] += 1;
@@ -1008,14 +1091,11 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
           if (__syncthreads_or(c1)) chg |= 1u << g;
         }
         F64_STAMP(3);
-        {
-          int na = 0;
-          for (int g = 0; g < G; ++g) na += (act >> g) & 1u;
-          msum_multi(w, par, na, s_gof, K, d, m, tid);
-        }
+        msum_multi(w, par, s_gof, s_jm, nJ, d, m, tid);
         F64_STAMP(4);
         for (int g = 0; g < G; ++g) {
           if (!((act >> g) & 1u)) continue;
+          const int K = s_K[g];
           const double* cen = w.cen_of(g, (par >> g) & 1u);
           double* cnew = w.cen_of(g, ((par >> g) & 1u) ^ 1u);
           const int32_t* lab = w.lab_of(g);
@@ -1132,7 +1212,7 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
             nit[g] = it + 1;
             continue;
           }
-          const double tot = np_pairwise(s_sh[g], K);
+          const double tot = np_pairwise(s_sh[g], s_K[g]);
           const int32_t* lab = w.lab_of(g);
           int32_t* lold = w.lold_of(g);
           for (int r = tid; r < m; r += NT) lold[r] = lab[r];
@@ -1145,18 +1225,19 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
       __syncthreads();
       const unsigned fin = ((1u << G) - 1u) & ~strict;  // final E-step against the last centres
       if (fin) {
-        for (int e = tid; e < G * K; e += NT) {
-          const int g = e / K, j = e - g * K;
+        for (int g = 0; g < G; ++g) {
           if (!((fin >> g) & 1u)) continue;
-          const double* cj = w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(j) * d;
-          s_cn[g][j] = einsum_sq([&](int k) { return cj[k]; }, d);
+          for (int j = tid; j < s_K[g]; j += NT) {
+            const double* cj = w.cen_of(g, (par >> g) & 1u) + static_cast<size_t>(j) * d;
+            s_cn[g][j] = einsum_sq([&](int k) { return cj[k]; }, d);
+          }
         }
         __syncthreads();
-        estep_multi(w, fin, par, G, &s_cn[0][0], K, d, m, s_gof, tid);
+        estep_multi<GM>(w, fin, par, G, s_K, &s_cn[0][0], s_cnp, d, m, s_gof, s_jm, tid);
       }
-      // inertia of every init of the group in one pass over the rows: per-row squared distance to
-      // its centre (into the init's free k-means++ buffer), then each init's row-order sum on the
-      // first thread of its own wave
+      // inertia of every problem of the group in one pass over the rows: per-row squared distance
+      // to its centre (into the problem's free k-means++ buffer), then each problem's row-order
+      // sum on its own walker thread
       for (int r = tid; r < m; r += NT) {
         const XfRow x(w, d, r);
         for (int g = 0; g < G; ++g) {
@@ -1178,29 +1259,33 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
         }
       }
       __syncthreads();
-      if ((tid & 63) == 0 && (tid >> 6) < G) {
-        // the row-order sum, its loads 16 rows ahead of the adds (one thread walking global
-        // memory otherwise waits a round trip per row)
-        const double* sq = w.dc_of(tid >> 6);
-        double sacc = 0.0;
-        int r = 0;
-        for (; r + 16 <= m; r += 16) {
-          double v[16];
+      {
+        const int gw = walker_slot(tid);
+        if (gw < G) {
+          // the row-order sum, its loads 16 rows ahead of the adds (one thread walking global
+          // memory otherwise waits a round trip per row)
+          const double* sq = w.dc_of(gw);
+          double sacc = 0.0;
+          int r = 0;
+          for (; r + 16 <= m; r += 16) {
+            double v[16];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) v[u] = sq[r + u];
+            for (int u = 0; u < 16; ++u) v[u] = sq[r + u];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) sacc += v[u];
+            for (int u = 0; u < 16; ++u) sacc += v[u];
+          }
+          for (; r < m; ++r) sacc += sq[r];
+          s_potg[gw] = sacc;
         }
-        for (; r < m; ++r) sacc += sq[r];
-        s_potg[tid >> 6] = sacc;
       }
       __syncthreads();
       for (int g = 0; g < G; ++g) {
         const int32_t* lab = w.lab_of(g);
         const double inertia = s_potg[g];
         const int n_iter = nit[g];
-        // best of n_init: lower inertia AND a different clustering
-        bool take = (g0 + g == 0);
+        const int ini = s_ini[g];
+        // best of n_init (per K, in init order): lower inertia AND a different clustering
+        bool take = (ini == 0);
         if (!take && inertia < best_inertia) {
           for (int j = tid; j <= KMAX; j += NT) s_map[j] = -1;
           __syncthreads();
@@ -1231,14 +1316,18 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
           best_iter = n_iter;
         }
         __syncthreads();
+        if (ini == a.n_init - 1) {  // this K's last init: its best clustering is final
+          const int kk = s_kk[g];
+          uint8_t* out = a.labels + static_cast<size_t>(kk) * a.n * a.ldl + h;
+          for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = w.lbest[r];
+          if (tid == 0) {
+            if (a.inertia_out) a.inertia_out[static_cast<size_t>(kk) * a.H + h] = best_inertia;
+            if (a.niter_out) a.niter_out[static_cast<size_t>(kk) * a.H + h] = best_iter;
+          }
+          __syncthreads();
+        }
       }
       F64_STAMP(6);
-    }
-    uint8_t* out = a.labels + static_cast<size_t>(kk) * a.n * a.ldl + h;
-    for (int r = tid; r < m; r += NT) out[static_cast<size_t>(idx[r]) * a.ldl] = w.lbest[r];
-    if (tid == 0) {
-      if (a.inertia_out) a.inertia_out[static_cast<size_t>(kk) * a.H + h] = best_inertia;
-      if (a.niter_out) a.niter_out[static_cast<size_t>(kk) * a.H + h] = best_iter;
     }
   }
 #ifdef CC_F64_STAMPS
@@ -1343,6 +1432,51 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   for (int i = 0; i < nK; ++i) a.Ks[i] = Ks[i];
   for (int i = 0; i < nK; ++i) a.korder[i] = i;
   std::stable_sort(a.korder, a.korder + nK, [&](int x, int y) { return Ks[x] > Ks[y]; });
+  // unit kinds: runs of up to P adjacent K's (in decreasing K) whose P * n_init problems fit one
+  // lockstep group, so each pass over a resample's rows serves several K's.  Only K <= kpair_max
+  // are grouped (the light units: their centre tiles are mostly empty and the per-unit setup
+  // dominates); the kinds are then dealt in decreasing total K (longest-processing-time order).
+  int P = std::max(1, std::min(F64_KPACK, GMAX / n_init));
+  // grouped K's make heavier units, and the launch's tail is about one unit long: group only where
+  // every workgroup gets several units (C2 H = 500: 1.10x; C3 H = 128, ~2.5 per workgroup: 0.96x)
+  if (P > 1) {
+    int dev = 0, cus = 0;  // resident workgroups: two per CU (the kernel's occupancy)
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = grid;
+    const long long resident = std::min<long long>(grid, 2LL * cus);
+    if (static_cast<long long>(nh) * ((nK + P - 1) / P) < F64_UNITS_PER_WG * resident) P = 1;
+  }
+  if (const char* ev = std::getenv("CCMI_F64_KPACK")) P = std::max(1, std::min(std::atoi(ev), GMAX / std::max(n_init, 1)));
+  int kpair_max = F64_KPAIR_MAX;
+  if (const char* ev = std::getenv("CCMI_F64_KPAIR_MAX")) kpair_max = std::atoi(ev);
+  {
+    int kinds[NKMAX][2], nk = 0;  // (first position in the sorted K order, count)
+    for (int i = 0; i < nK;) {
+      int c = 1;
+      if (Ks[a.korder[i]] <= kpair_max)
+        while (c < P && i + c < nK) ++c;
+      kinds[nk][0] = i;
+      kinds[nk][1] = c;
+      ++nk;
+      i += c;
+    }
+    auto wt = [&](int u) {
+      int s = 0;
+      for (int q = 0; q < kinds[u][1]; ++q) s += Ks[a.korder[kinds[u][0] + q]];
+      return s;
+    };
+    int ord[NKMAX];
+    for (int u = 0; u < nk; ++u) ord[u] = u;
+    std::stable_sort(ord, ord + nk, [&](int x, int y) { return wt(x) > wt(y); });
+    int ko[NKMAX], pos = 0;
+    a.nuk = nk;
+    for (int u = 0; u < nk; ++u) {
+      a.ukfirst[u] = pos;
+      for (int q = 0; q < kinds[ord[u]][1]; ++q) ko[pos++] = a.korder[kinds[ord[u]][0] + q];
+    }
+    a.ukfirst[nk] = pos;
+    for (int i = 0; i < nK; ++i) a.korder[i] = ko[i];
+  }
   a.n_init = n_init;
   a.max_iter = max_iter;
   a.tol_rel = tol_rel;
@@ -1371,7 +1505,7 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.o_cf = L.o_cf;
   a.kd = static_cast<size_t>(kmax) * d;
   a.cfs = L.cfs;
-  const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * nK));
+  const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * a.nuk));
   // one upload: the zeroed counter and the arguments (a pageable source is consumed before
   // hipMemcpyAsync returns)
   alignas(16) unsigned char header[WS_ARGS + sizeof(F64Args)] = {};
@@ -1381,8 +1515,9 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
     cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));
     return CC_ERR_HIP;
   }
-  hipLaunchKernelGGL(kmeans_f64_kernel, dim3(blocks), dim3(NT), 0, st,
-                     reinterpret_cast<const F64Args*>(static_cast<char*>(workspace) + WS_ARGS));
+  const F64Args* pa = reinterpret_cast<const F64Args*>(static_cast<char*>(workspace) + WS_ARGS);
+  if (P * n_init > 4) hipLaunchKernelGGL(kmeans_f64_kernel<GMAX>, dim3(blocks), dim3(NT), 0, st, pa);
+  else hipLaunchKernelGGL(kmeans_f64_kernel<4>, dim3(blocks), dim3(NT), 0, st, pa);
   e = hipGetLastError();
   if (e != hipSuccess) {
     cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));

@@ -252,6 +252,36 @@ def test_f64_labels_match_sklearn_float64(n, d, k_true, Ks, H):
     assert exact >= 0.9 * (exact + ill), (exact, ill)
 
 
+@pytest.mark.parametrize("n_init", [1, 2, 3])
+def test_f64_two_k_units_identical_to_one_k_units(n_init, monkeypatch):
+    """cc_kmeans_f64 units of two adjacent K's (their problems share every pass over the rows;
+    chosen by the host when every workgroup gets several units) give the same labels, inertia and
+    n_iter as units of one K, bit for bit.  CCMI_F64_KPACK forces either grouping; n_init = 3 runs
+    the 6-problem groups (K = 127 and 100 together: 36 k-means++ candidates, three tiles)."""
+    seed = 5
+    n, d, H = 700, 24, 5
+    X = blobs(n, d, 4, seed=11).astype(np.float64)
+    X += np.random.default_rng(1).normal(scale=0.5, size=X.shape)
+    Ks = [2, 3, 5, 8, 13, 20, 100, 127]
+    dev = engine.require_gpu()
+    m = int(0.8 * n)
+    idx_d = torch.from_numpy(engine.resample_indices(seed, n, m, 0, H)).to(dev)
+    X64 = torch.from_numpy(X).to(dev)
+    out = {}
+    for P in ("1", "2"):
+        monkeypatch.setenv("CCMI_F64_KPACK", P)
+        L = engine.new_label_matrix(len(Ks), n, engine.pad_h(H), dev)
+        inert = torch.zeros((len(Ks), H), dtype=torch.float64, device=dev)
+        nit = torch.zeros((len(Ks), H), dtype=torch.int32, device=dev)
+        BatchedKMeans(Ks, n_init=n_init, random_state=seed).run_f64(
+            X64, idx_d, n, H, m, 0, H, L, inertia=inert, n_iter=nit)
+        torch.cuda.synchronize()
+        out[P] = (L.cpu().numpy(), inert.cpu().numpy(), nit.cpu().numpy())
+    assert np.all(out["1"][1] > 0) and np.all(out["1"][2] >= 1)
+    for a, b in zip(out["1"], out["2"]):
+        np.testing.assert_array_equal(a, b)
+
+
 
 def test_f64_c3_shape_identical_to_sklearn_float64():
     """float64 input at the C3 shape (n = 50 000, m = 40 000, d = 128, K = 2..20, 2 resamples;
