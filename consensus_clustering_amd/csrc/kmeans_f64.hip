@@ -24,11 +24,16 @@
 //
 // Mapping: a persistent grid; one 256-thread workgroup runs one (resample, K) unit at a time,
 // units dealt in decreasing K, with per-workgroup float64 scratch in the caller's workspace.
+// Each resample's centred rows, their fragment image, row norms and tol are built once, by two
+// setup kernels before the units' launch, into per-resample slots of the workspace (up to grid
+// resamples per launch); a unit of two adjacent K's (where units are plentiful) runs both K's
+// problems in one lockstep group.
 // Round 5: a unit's inits run in lockstep groups of up to GMAX (each pass over the rows - the
 // k-means++ distances, the E-step, the centre sums, the inertia - serves every running init of
 // the group; an init that converges leaves the group), and the centre sums accumulate in LDS
 // where they fit; every init's values and orders are those of a run on its own.
-// Round 4: the unit's centred rows are materialised once ([m][d] float64, the same subtraction),
+// Round 4: the unit's centred rows are materialised once ([m][d] float64, the same subtraction;
+// round 5: once per resample),
 // every dot product runs as one of G (or ntr) independent sequential FMA chains per thread (a
 // thread's row against G centres at once: the same chain per value, G times the ILP), and the
 // centre sums walk per-cluster row lists built in row order (a ballot compaction), one thread
@@ -88,8 +93,11 @@ struct F64Args {
   unsigned* counter;
   char* ws;
   size_t per_wg;
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf, o_cf;
+  size_t o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_cf;
   size_t kd, cfs;  // per-init strides (doubles) of the centres and of their operand images
+  // per-resample images (slot hb of this launch's resamples), built once by the setup kernels
+  char* rs;
+  size_t per_res, r_mean, r_var, r_tol, r_xsq, r_xc, r_xf;
 };
 
 // numpy pairwise_sum (numpy/_core/src/umath/loops_utils.h.src) of a contiguous double array:
@@ -834,6 +842,91 @@ __device__ __forceinline__ double xc(const F64Args& a, const int32_t* idx, const
   return a.X[static_cast<size_t>(idx[r]) * a.d + k] - mean[k];
 }
 
+// ---- per-resample setup (KMeans.fit's centring and _tolerance, once per resample) -----------
+// Thread (slot, feature k): the column mean of the resample's rows (rows in order), then the
+// variance of the centred column, the loads of 16 rows in flight ahead of the adds.
+__global__ __launch_bounds__(NT) void f64_setup_stats(const F64Args* __restrict__ pa) {
+  const F64Args& a = *pa;
+  const int d = a.d, m = a.m;
+  const long long e = static_cast<long long>(blockIdx.x) * NT + threadIdx.x;
+  if (e >= static_cast<long long>(a.nh) * d) return;
+  const int hb = static_cast<int>(e / d), k = static_cast<int>(e - static_cast<long long>(hb) * d);
+  const int32_t* idx = a.idx + static_cast<size_t>(a.h_begin + hb) * m;
+  char* rb = a.rs + static_cast<size_t>(hb) * a.per_res;
+  double s = 0.0;
+  int r = 0;
+  for (; r + 16 <= m; r += 16) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = a.X[static_cast<size_t>(idx[r + u]) * d + k];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
+  for (; r < m; ++r) s += a.X[static_cast<size_t>(idx[r]) * d + k];
+  const double mu = s / m;
+  double q = 0.0;
+  for (r = 0; r + 16 <= m; r += 16) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = a.X[static_cast<size_t>(idx[r + u]) * d + k] - mu;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) q += v[u] * v[u];
+  }
+  for (; r < m; ++r) {
+    const double t = a.X[static_cast<size_t>(idx[r]) * d + k] - mu;
+    q += t * t;
+  }
+  reinterpret_cast<double*>(rb + a.r_mean)[k] = mu;
+  reinterpret_cast<double*>(rb + a.r_var)[k] = q / m;
+}
+
+constexpr int SRT = 4;  // row tiles of 16 per setup workgroup
+
+// Workgroup (slot, block of SRT row tiles): the centred rows X[idx[r]][k] - mean[k] (rounded
+// once), the same values as the matrix cores' B operand image (row tile t, k-step s, lane l
+// holds row 16t + (l & 15), feature 4s + (l >> 4); exact zeros past m and d, so every operand
+// load of a k-step is one contiguous 512-B piece), the rows' squared norms (einsum order); block 0
+// also tol = mean(var) * tol_rel (_tolerance: numpy pairwise mean over the features).
+__global__ __launch_bounds__(NT) void f64_setup_rows(const F64Args* __restrict__ pa, int nrb) {
+  const F64Args& a = *pa;
+  const int d = a.d, m = a.m, tid = threadIdx.x;
+  const int hb = blockIdx.x / nrb, rbk = blockIdx.x - hb * nrb;
+  const int32_t* idx = a.idx + static_cast<size_t>(a.h_begin + hb) * m;
+  char* rb = a.rs + static_cast<size_t>(hb) * a.per_res;
+  const double* mean = reinterpret_cast<const double*>(rb + a.r_mean);
+  double* xcp = reinterpret_cast<double*>(rb + a.r_xc);
+  double* xf = reinterpret_cast<double*>(rb + a.r_xf);
+  double* xsq = reinterpret_cast<double*>(rb + a.r_xsq);
+  if (rbk == 0 && tid == 0) {
+    const double* var = reinterpret_cast<const double*>(rb + a.r_var);
+    *reinterpret_cast<double*>(rb + a.r_tol) = (np_pairwise(var, d) / d) * a.tol_rel;
+  }
+  const int r0 = rbk * SRT * 16, r1 = r0 + SRT * 16 < m ? r0 + SRT * 16 : m;
+  for (int r = r0; r < r1; ++r) {
+    const double* xr = a.X + static_cast<size_t>(idx[r]) * d;
+    for (int k = tid; k < d; k += NT) xcp[static_cast<size_t>(r) * d + k] = xr[k] - mean[k];
+  }
+  __syncthreads();
+  const int S4 = (d + 3) >> 2;
+  const int ntl = (m + 15) >> 4;
+  const int l = tid & 63, wv = tid >> 6;
+  const int rl = l & 15, kl = l >> 4;
+  for (int t = rbk * SRT; t < ntl && t < (rbk + 1) * SRT; ++t) {
+    const int r = 16 * t + rl;
+    for (int sk = wv; sk < S4; sk += NT / 64) {
+      const int k = 4 * sk + kl;
+      xf[(static_cast<size_t>(t) * S4 + sk) * 64 + l] = (r < m && k < d) ? xcp[static_cast<size_t>(r) * d + k] : 0.0;
+    }
+  }
+  __syncthreads();
+  WG w;
+  w.xf = xf;
+  for (int r = r0 + tid; r < r1; r += NT) {
+    const XfRow x(w, d, r);
+    xsq[r] = einsum_sq([&](int k) { return x[k]; }, d);
+  }
+}
+
 template <int GM>
 __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __restrict__ pa) {
   // arguments read from the workspace header (as in kmeans.hip): re-loaded where used rather
@@ -858,8 +951,6 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   const int tid = threadIdx.x;
   char* base = a.ws + static_cast<size_t>(blockIdx.x) * a.per_wg;
   WG w;
-  w.mean = reinterpret_cast<double*>(base + a.o_mean);
-  w.xsq = reinterpret_cast<double*>(base + a.o_xsq);
   w.cl = reinterpret_cast<double*>(base + a.o_cl);
   w.dc = reinterpret_cast<double*>(base + a.o_dc);
   w.sq = reinterpret_cast<double*>(base + a.o_sq);
@@ -868,8 +959,6 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
   w.lab = reinterpret_cast<int32_t*>(base + a.o_lab);
   w.lold = reinterpret_cast<int32_t*>(base + a.o_lold);
   w.lbest = reinterpret_cast<uint8_t*>(base + a.o_lbest);
-  w.xc = reinterpret_cast<double*>(base + a.o_xc);
-  w.xf = reinterpret_cast<double*>(base + a.o_xf);
   w.cf = reinterpret_cast<double*>(base + a.o_cf);
   const int m = a.m, d = a.d;
   w.m = m;
@@ -898,81 +987,15 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
     const int h = a.h_begin + hb;
     const int32_t* idx = a.idx + static_cast<size_t>(h) * m;
 
-    // column means (rows in order), then variances of the centred columns
-    for (int k = tid; k < d; k += NT) {
-      // sums in row order, the loads of 8 rows in flight ahead of the adds
-      double s = 0.0;
-      int r = 0;
-      for (; r + 8 <= m; r += 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = a.X[static_cast<size_t>(idx[r + u]) * d + k];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
-      }
-      for (; r < m; ++r) s += a.X[static_cast<size_t>(idx[r]) * d + k];
-      const double mu = s / m;
-      double q = 0.0;
-      for (r = 0; r + 8 <= m; r += 8) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = a.X[static_cast<size_t>(idx[r + u]) * d + k] - mu;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) q += v[u] * v[u];
-      }
-      for (; r < m; ++r) {
-        const double t = a.X[static_cast<size_t>(idx[r]) * d + k] - mu;
-        q += t * t;
-      }
-      w.mean[k] = mu;
-      w.sq[k] = q / m;  // var (sq is free until the E-steps)
-    }
-    __syncthreads();
-    if (tid == 0) s_tol = (np_pairwise(w.sq, d) / d) * a.tol_rel;
-    // the centred rows, once per unit (the values every later step reads): a thread keeps one
-    // feature and walks rows NT / d apart, four rows' gathers in flight (no 64-bit index division)
-    if (d <= NT) {
-      const int rpi = NT / d, rr = tid / d, kk = tid - (tid / d) * d;
-      if (rr < rpi) {
-        const double mu = w.mean[kk];
-        int r = rr;
-        for (; r + 3 * rpi < m; r += 4 * rpi) {
-          double v[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) v[u] = a.X[static_cast<size_t>(idx[r + u * rpi]) * d + kk];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) w.xc[static_cast<size_t>(r + u * rpi) * d + kk] = v[u] - mu;
-        }
-        for (; r < m; r += rpi) w.xc[static_cast<size_t>(r) * d + kk] = xc(a, idx, w.mean, r, kk);
-      }
-    } else {
-      for (int r = 0; r < m; ++r)
-        for (int k = tid; k < d; k += NT) w.xc[static_cast<size_t>(r) * d + k] = xc(a, idx, w.mean, r, k);
-    }
-    __syncthreads();
-    // the same values as the matrix cores' B operand image: row tile t, k-step s, lane l holds
-    // row 16t + (l & 15), feature 4s + (l >> 4) (exact zeros past m and d), so every operand
-    // load of a k-step is one contiguous 512-B piece; wave w writes the pieces (t, s) with
-    // t * S4 + s = w mod NT / 64
+    // the resample's centred rows, their fragment image and norms, and tol: built once per
+    // resample by the setup kernels
     {
-      const int S4 = (d + 3) >> 2;
-      const int ntl = (m + 15) >> 4;
-      const int l = tid & 63, wv = tid >> 6;
-      const int rl = l & 15, kl = l >> 4;
-      for (int t = 0; t < ntl; ++t) {
-        const int r = 16 * t + rl;
-        for (int sk = (wv - t * S4 % (NT / 64) + (NT / 64)) % (NT / 64); sk < S4; sk += NT / 64) {
-          const int k = 4 * sk + kl;
-          w.xf[(static_cast<size_t>(t) * S4 + sk) * 64 + l] =
-              (r < m && k < d) ? w.xc[static_cast<size_t>(r) * d + k] : 0.0;
-        }
-      }
-    }
-    __syncthreads();
-    // squared row norms of the centred rows
-    for (int r = tid; r < m; r += NT) {
-      const XfRow x(w, d, r);
-      w.xsq[r] = einsum_sq([&](int k) { return x[k]; }, d);
+      char* rb = a.rs + static_cast<size_t>(hb) * a.per_res;
+      w.mean = reinterpret_cast<double*>(rb + a.r_mean);
+      w.xsq = reinterpret_cast<double*>(rb + a.r_xsq);
+      w.xc = reinterpret_cast<double*>(rb + a.r_xc);
+      w.xf = reinterpret_cast<double*>(rb + a.r_xf);
+      if (tid == 0) s_tol = *reinterpret_cast<const double*>(rb + a.r_tol);
     }
     __syncthreads();
     F64_STAMP(0);
@@ -1338,17 +1361,18 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
 #endif
 }
 
+// The workspace after its header: grid per-workgroup areas, then grid per-resample slots (a
+// launch takes up to grid resamples at a time).
 struct F64Layout {
-  size_t o_mean, o_xsq, o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_xc, o_xf, o_cf, per_wg;
+  size_t o_cl, o_dc, o_sq, o_cen, o_cnew, o_lab, o_lold, o_lbest, o_cf, per_wg;
   size_t cfs;
+  size_t r_mean, r_var, r_tol, r_xsq, r_xc, r_xf, per_res;
 };
 
 F64Layout f64_layout(int m, int d, int kmax) {
   auto al = [](size_t x) { return (x + 255) & ~static_cast<size_t>(255); };
   F64Layout L{};
   size_t o = 0;
-  L.o_mean = o;  o += al(sizeof(double) * std::max(d, 1));
-  L.o_xsq = o;   o += al(sizeof(double) * m);
   L.o_cl = o;    o += al(sizeof(double) * m * GMAX);
   L.o_dc = o;    o += al(sizeof(double) * m * TMAX * GMAX);
   L.o_sq = o;    o += al(sizeof(double) * std::max(m, d));
@@ -1357,11 +1381,17 @@ F64Layout f64_layout(int m, int d, int kmax) {
   L.o_lab = o;   o += al(sizeof(int32_t) * m * GMAX);
   L.o_lold = o;  o += al(sizeof(int32_t) * m * GMAX);
   L.o_lbest = o; o += al(m);
-  L.o_xc = o;    o += al(sizeof(double) * static_cast<size_t>(m) * d);
-  L.o_xf = o;    o += al(sizeof(double) * static_cast<size_t>((m + 15) / 16) * 16 * ((d + 3) / 4) * 4);
   L.cfs = static_cast<size_t>(std::max((kmax + 31) / 32, 1)) * 32 * ((d + 3) / 4) * 4;  // >= GMAX * TMAX rows
   L.o_cf = o;    o += al(sizeof(double) * L.cfs * GMAX);
   L.per_wg = o;
+  o = 0;
+  L.r_mean = o;  o += al(sizeof(double) * d);
+  L.r_var = o;   o += al(sizeof(double) * d);
+  L.r_tol = o;   o += al(sizeof(double));
+  L.r_xsq = o;   o += al(sizeof(double) * m);
+  L.r_xc = o;    o += al(sizeof(double) * static_cast<size_t>(m) * d);
+  L.r_xf = o;    o += al(sizeof(double) * static_cast<size_t>((m + 15) / 16) * 16 * ((d + 3) / 4) * 4);
+  L.per_res = o;
   return L;
 }
 
@@ -1383,7 +1413,8 @@ extern "C" size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks,
   if (m <= 0 || d <= 0 || !Ks || nK <= 0 || grid <= 0) return 0;
   int kmax = 1;
   for (int i = 0; i < nK; ++i) kmax = std::max(kmax, Ks[i]);
-  return WS_HEADER + f64_layout(m, d, kmax).per_wg * static_cast<size_t>(grid);
+  const F64Layout L = f64_layout(m, d, kmax);
+  return WS_HEADER + (L.per_wg + L.per_res) * static_cast<size_t>(grid);
 }
 
 extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_hm, int H, int m,
@@ -1414,7 +1445,7 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   const int nh = h_end - h_begin;
   if (nh == 0) return CC_OK;
   const F64Layout L = f64_layout(m, d, kmax);
-  if (!workspace || ws_bytes < WS_HEADER + L.per_wg * static_cast<size_t>(grid)) {
+  if (!workspace || ws_bytes < WS_HEADER + (L.per_wg + L.per_res) * static_cast<size_t>(grid)) {
     cc::set_error("cc_kmeans_f64: workspace too small");
     return CC_ERR_ARG;
   }
@@ -1444,7 +1475,7 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = grid;
     const long long resident = std::min<long long>(grid, 2LL * cus);
-    if (static_cast<long long>(nh) * ((nK + P - 1) / P) < F64_UNITS_PER_WG * resident) P = 1;
+    if (static_cast<long long>(std::min(nh, grid)) * ((nK + P - 1) / P) < F64_UNITS_PER_WG * resident) P = 1;
   }
   if (const char* ev = std::getenv("CCMI_F64_KPACK")) P = std::max(1, std::min(std::atoi(ev), GMAX / std::max(n_init, 1)));
   int kpair_max = F64_KPAIR_MAX;
@@ -1490,8 +1521,6 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.counter = static_cast<unsigned*>(workspace);
   a.ws = static_cast<char*>(workspace) + WS_HEADER;
   a.per_wg = L.per_wg;
-  a.o_mean = L.o_mean;
-  a.o_xsq = L.o_xsq;
   a.o_cl = L.o_cl;
   a.o_dc = L.o_dc;
   a.o_sq = L.o_sq;
@@ -1500,28 +1529,43 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   a.o_lab = L.o_lab;
   a.o_lold = L.o_lold;
   a.o_lbest = L.o_lbest;
-  a.o_xc = L.o_xc;
-  a.o_xf = L.o_xf;
   a.o_cf = L.o_cf;
   a.kd = static_cast<size_t>(kmax) * d;
   a.cfs = L.cfs;
-  const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(nh) * a.nuk));
-  // one upload: the zeroed counter and the arguments (a pageable source is consumed before
-  // hipMemcpyAsync returns)
-  alignas(16) unsigned char header[WS_ARGS + sizeof(F64Args)] = {};
-  std::memcpy(header + WS_ARGS, &a, sizeof(F64Args));
-  hipError_t e = hipMemcpyAsync(workspace, header, sizeof(header), hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) {
-    cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));
-    return CC_ERR_HIP;
-  }
+  a.rs = a.ws + L.per_wg * static_cast<size_t>(grid);
+  a.per_res = L.per_res;
+  a.r_mean = L.r_mean;
+  a.r_var = L.r_var;
+  a.r_tol = L.r_tol;
+  a.r_xsq = L.r_xsq;
+  a.r_xc = L.r_xc;
+  a.r_xf = L.r_xf;
   const F64Args* pa = reinterpret_cast<const F64Args*>(static_cast<char*>(workspace) + WS_ARGS);
-  if (P * n_init > 4) hipLaunchKernelGGL(kmeans_f64_kernel<GMAX>, dim3(blocks), dim3(NT), 0, st, pa);
-  else hipLaunchKernelGGL(kmeans_f64_kernel<4>, dim3(blocks), dim3(NT), 0, st, pa);
-  e = hipGetLastError();
-  if (e != hipSuccess) {
-    cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));
-    return CC_ERR_HIP;
+  const int nrb = ((m + 15) / 16 + SRT - 1) / SRT;
+  // up to grid resamples per launch (the per-resample slots): their setup, then their units
+  const int chunk = std::min(nh, grid);
+  for (int c0 = 0; c0 < nh; c0 += chunk) {
+    const int cn = std::min(chunk, nh - c0);
+    a.h_begin = h_begin + c0;
+    a.nh = cn;
+    // one upload: the zeroed counter and the arguments (a pageable source is consumed before
+    // hipMemcpyAsync returns; the previous launches read theirs first, in stream order)
+    alignas(16) unsigned char header[WS_ARGS + sizeof(F64Args)] = {};
+    std::memcpy(header + WS_ARGS, &a, sizeof(F64Args));
+    hipError_t e = hipMemcpyAsync(workspace, header, sizeof(header), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+      const long long nst = (static_cast<long long>(cn) * d + NT - 1) / NT;
+      hipLaunchKernelGGL(f64_setup_stats, dim3(static_cast<unsigned>(nst)), dim3(NT), 0, st, pa);
+      hipLaunchKernelGGL(f64_setup_rows, dim3(static_cast<unsigned>(cn) * nrb), dim3(NT), 0, st, pa, nrb);
+      const unsigned blocks = static_cast<unsigned>(std::min<long long>(grid, static_cast<long long>(cn) * a.nuk));
+      if (P * n_init > 4) hipLaunchKernelGGL(kmeans_f64_kernel<GMAX>, dim3(blocks), dim3(NT), 0, st, pa);
+      else hipLaunchKernelGGL(kmeans_f64_kernel<4>, dim3(blocks), dim3(NT), 0, st, pa);
+      e = hipGetLastError();
+    }
+    if (e != hipSuccess) {
+      cc::set_error(std::string("cc_kmeans_f64: ") + hipGetErrorString(e));
+      return CC_ERR_HIP;
+    }
   }
   return CC_OK;
 }
