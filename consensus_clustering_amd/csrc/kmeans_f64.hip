@@ -234,6 +234,8 @@ __device__ double blas_gemv_t_ones(const double* x, int m, int col, int ncol) {
 // the units' phases.
 #ifdef CC_F64_STAMPS
 __device__ unsigned long long cc_f64_stamps[16];
+constexpr int F64_UT = 16384;                        // units with recorded times
+__device__ unsigned long long cc_f64_utimes[F64_UT][3];  // per unit: start, end, workgroup
 #define F64_STAMP(ph)                               \
   do {                                              \
     if (tid == 0) {                                 \
@@ -979,6 +981,12 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
     const int unit = s_unit;
     if (unit >= a.nh * a.nuk) break;
     F64_STAMP(7);
+#ifdef CC_F64_STAMPS
+    if (tid == 0 && unit < F64_UT) {
+      cc_f64_utimes[unit][0] = wall_clock64();
+      cc_f64_utimes[unit][2] = blockIdx.x;
+    }
+#endif
     // unit kinds in decreasing K, every resample's unit of the heaviest kind first: the longest
     // units start first and the short ones fill the tail (longest-processing-time order).  A kind
     // is one K or a run of adjacent K's (korder[kf .. kf + P)) whose problems share the passes.
@@ -1352,6 +1360,9 @@ __global__ __launch_bounds__(NT, 2) void kmeans_f64_kernel(const F64Args* __rest
       }
       F64_STAMP(6);
     }
+#ifdef CC_F64_STAMPS
+    if (tid == 0 && unit < F64_UT) cc_f64_utimes[unit][1] = wall_clock64();
+#endif
   }
 #ifdef CC_F64_STAMPS
   if (tid == 0) {
@@ -1402,6 +1413,13 @@ constexpr size_t WS_HEADER = (WS_ARGS + sizeof(F64Args) + 255) / 256 * 256;
 
 #ifdef CC_F64_STAMPS
 // the accumulated stamps (then zeroed): [0..7] phase clocks, [8] Lloyd iterations, [9] workgroups
+// per-unit wall clocks of the last launch (start, end, workgroup), units < n
+extern "C" int cc_kmeans_f64_unit_times(unsigned long long* out, int n) {
+  n = std::min(n, F64_UT);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cc_f64_utimes), static_cast<size_t>(n) * 3 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -1;
+}
+
 extern "C" int cc_kmeans_f64_stamps(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(cc_f64_stamps), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
   const unsigned long long z[16] = {};

@@ -52,4 +52,30 @@ for i in range(0, len(args), 2):
     for q in list(range(8)) + [10, 11, 12]:
         name = NAMES[q] if q < 8 else ["  k-means++ search", "  k-means++ distances", "  k-means++ potentials"][q - 10]
         print(f"  {name:22s} {100 * out[q] / tot:5.1f} %   {out[q] / 100e3 / max(int(out[9]), 1):9.1f} ms per workgroup")
+    # per-unit timeline of the launch (units dealt in order: kind-major, resample-minor)
+    nu = H * len(cfg["Ks"])
+    ut = np.zeros((nu, 3), dtype=np.uint64)
+    if hasattr(lib, "cc_kmeans_f64_unit_times") and nu <= 16384:
+        lib.cc_kmeans_f64_unit_times(ctypes.c_void_p(ut.ctypes.data), nu)
+        used = ut[:, 1] > 0
+        ut = ut[used].astype(np.float64)
+        t0 = ut[:, 0].min()
+        st, en = (ut[:, 0] - t0) / 100e3, (ut[:, 1] - t0) / 100e3
+        dur = en - st
+        wall = en.max()
+        ends = np.array([en[ut[:, 2] == w].max() for w in np.unique(ut[:, 2])])
+        print(f"  timeline: {int(used.sum())} units, last end {wall:.1f} ms; workgroup finish "
+              f"p10/p50/p90 {np.percentile(ends, 10):.1f}/{np.percentile(ends, 50):.1f}/"
+              f"{np.percentile(ends, 90):.1f} ms; busy {100 * dur.sum() / (len(ends) * wall):.1f} %")
+        order = np.argsort(-dur)[:8]
+        print("  longest units (index, start, duration ms): " +
+              ", ".join(f"{np.flatnonzero(used)[i]}@{st[i]:.0f}+{dur[i]:.0f}" for i in order))
+        late = np.argsort(-st)[:5]
+        print("  last started (index, start, duration ms): " +
+              ", ".join(f"{np.flatnonzero(used)[i]}@{st[i]:.0f}+{dur[i]:.0f}" for i in late))
+        # mean duration per unit kind (rows of H consecutive units)
+        idx_used = np.flatnonzero(used)
+        kinds = idx_used // H
+        print("  per kind mean/max ms: " + " ".join(
+            f"{k}:{dur[kinds == k].mean():.0f}/{dur[kinds == k].max():.0f}" for k in np.unique(kinds)))
     sys.stdout.flush()
