@@ -69,7 +69,7 @@ constexpr int NKMAX = 64;
 constexpr int GMAX = 6;
 constexpr int F64_KPACK = 2;        // K's per unit (at most GMAX / n_init)
 constexpr int F64_KPAIR_MAX = 127;  // only K's up to this are grouped
-constexpr int F64_UNITS_PER_WG = 4;  // ... and only with at least this many units per workgroup
+constexpr int F64_UNITS_PER_WG = 2;  // ... and only with at least this many units per workgroup
 
 struct F64Args {
   const double* X;  // [n][d] (not centred)
@@ -1487,7 +1487,8 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   // dominates); the kinds are then dealt in decreasing total K (longest-processing-time order).
   int P = std::max(1, std::min(F64_KPACK, GMAX / n_init));
   // grouped K's make heavier units, and the launch's tail is about one unit long: group only where
-  // every workgroup gets several units (C2 H = 500: 1.10x; C3 H = 128, ~2.5 per workgroup: 0.96x)
+  // every workgroup gets a few units (with the per-resample setup, against one K per unit: C2
+  // H = 500 1.13x, C3 H = 512 1.12x, C3 H = 128 at ~2.5 units per workgroup 1.03x)
   if (P > 1) {
     int dev = 0, cus = 0;  // resident workgroups: two per CU (the kernel's occupancy)
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
