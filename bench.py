@@ -177,6 +177,41 @@ def cpu_baseline(cfg, X, H_sample=8):
     }
 
 
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured float4 copy)
+
+
+def consensus_roofline(dev, n, H, reps=5):
+    """cc_consensus (K4, CC.py:372-373: C = f32(M) / f32(I + 1e-6), diag 1) on n x n int32 M and I
+    resident in HBM, the pass that runs whenever cij or predict is asked for: 12 algorithmic bytes
+    per element (two int32 reads, one float32 write) / the average launch time (HIP events on the
+    launch stream), against the 8 TB/s HBM peak.  Measured after the timed fits, outside them."""
+    from consensus_clustering_amd import engine
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    I = torch.randint(H // 2, H + 1, (n, n), dtype=torch.int32, device=dev, generator=g)
+    M = (I.to(torch.float32) * torch.rand((n, n), device=dev, generator=g)).to(torch.int32)
+    engine.consensus(M, I)  # warm-up (and the allocation of C)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record()
+        C = engine.consensus(M, I)
+        b.record()
+        del C
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in evs) / reps
+    nbytes = 12.0 * n * n
+    achieved = nbytes / (ms * 1e-3) / 1e9
+    del M, I
+    torch.cuda.empty_cache()
+    return {"kernel": "cc_consensus", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": checked_frac(achieved, HBM_PEAK_GBS, "consensus"),
+            "traffic": None, "n": n, "bytes_per_launch": nbytes, "avg_launch_ms": ms,
+            "note": "K4 C = M / (I + 1e-6) over n x n int32 M, I (12 B per element); runs when "
+                    "keep_matrices or predict asks for C, not inside the timed fit"}
+
+
 def usable_cores() -> int:
     """CPUs this process may use: its affinity mask, capped by the cgroup CPU quota (a GPU box
     shows every host CPU in the mask but grants one GPU's share of them)."""
@@ -252,6 +287,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-consensus-roofline", action="store_true")
     ap.add_argument("--H", type=int, default=None, help="override n_iterations (debug runs)")
     ap.add_argument("--rehearse", default=None, metavar="R/N",
                     help="one-GPU rehearsal of rank R's share of an N-GPU fit (exchanges skipped; "
@@ -420,6 +456,9 @@ def main():
             "fit_timings_s": {k: round(v, 4) for k, v in cc.timings_.items()},
             "partial": bool(cc.partial_),
         }
+        if world == 1 and not args.no_consensus_roofline and not args.rehearse:
+            # M, I and C at the config's n, capped at 50 000 (30 GB; C5's n would need 480 GB)
+            out["roofline_consensus"] = consensus_roofline(dev, min(cfg["n"], 50_000), cfg["H"])
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, X)
         print(json.dumps(out), flush=True)

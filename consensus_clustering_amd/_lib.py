@@ -59,7 +59,7 @@ SIGNATURES = {
     "cc_linkage_mst_workspace_bytes": (ctypes.c_size_t, [_c_int]),
     "cc_linkage_mst": (_c_int, [_vp, _c_int, _vp, _vp, ctypes.c_size_t, _vp]),
     "cc_linkage_check": (_c_int, [_vp, ctypes.c_size_t, _vp]),
-    "cc_kmeans_f64_workspace_bytes": (_c_sz, [_c_int, _c_int, _vp, _c_int, _c_int]),
+    "cc_kmeans_f64_workspace_bytes": (_c_sz, [_c_int, _c_int, _vp, _c_int, _c_int, _c_int]),
     "cc_kmeans_f64": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp,
                                _c_int, _c_int, _c_int, _c_dbl, _vp, _c_int, _vp, _vp, _c_int, _vp,
                                _vp, _vp, _c_sz, _c_int, _vp]),

@@ -38,7 +38,7 @@ import torch
 
 from . import dist, engine, post
 from ._hostfit import fit_predict_chunk, fit_predict_one
-from .kmeans import DEFAULT_WORKSPACE_BUDGET, BatchedKMeans
+from .kmeans import BatchedKMeans
 
 KMAX = 127  # largest K: uint8 labels (0xFF = not sampled) and int8 one-hot channels
 
@@ -84,7 +84,7 @@ class ConsensusClustering:
         *,
         keep_matrices='auto',
         device=None,
-        workspace_budget=DEFAULT_WORKSPACE_BUDGET,
+        workspace_budget=None,
         precision='auto',
         resampling='auto',
     ):

@@ -1031,6 +1031,50 @@ __global__ void copy_label_columns_kernel(const uint8_t* __restrict__ src, int64
   }
 }
 
+// C = f32(M) / f32(f64(I) + 1e-6), C_ii = 1 (CC.py:372-373), one HBM stream of 12 bytes per
+// element.  n % 4 == 0 (every row 16-B aligned): a workgroup per row (grid-stride over rows), each
+// thread 4 elements per access (dwordx4 loads of M and I, one dwordx4 store), 4 accesses in flight;
+// no per-element index division.  Otherwise the flat form below.
+typedef int cc_i4 __attribute__((ext_vector_type(4)));
+typedef float cc_f4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(256) consensus_rows_kernel(const int32_t* __restrict__ M,
+                                                             const int32_t* __restrict__ I, int n,
+                                                             float* __restrict__ C) {
+  constexpr int U = 4;
+  const int nv = n >> 2;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const size_t rb = static_cast<size_t>(i) * static_cast<size_t>(nv);
+    const cc_i4* Mr = reinterpret_cast<const cc_i4*>(M) + rb;
+    const cc_i4* Ir = reinterpret_cast<const cc_i4*>(I) + rb;
+    cc_f4* Cr = reinterpret_cast<cc_f4*>(C) + rb;
+    for (int v0 = threadIdx.x; v0 < nv; v0 += U * 256) {
+      cc_i4 mv[U], iv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int v = v0 + u * 256;
+        if (v < nv) {
+          mv[u] = __builtin_nontemporal_load(Mr + v);
+          iv[u] = __builtin_nontemporal_load(Ir + v);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int v = v0 + u * 256;
+        if (v < nv) {
+          cc_f4 c;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float fi = static_cast<float>(static_cast<double>(iv[u][q]) + 1e-6);
+            c[q] = (4 * v + q == i) ? 1.0f : static_cast<float>(mv[u][q]) / fi;
+          }
+          __builtin_nontemporal_store(c, Cr + v);
+        }
+      }
+    }
+  }
+}
+
 __global__ void consensus_kernel(const int32_t* __restrict__ M, const int32_t* __restrict__ I,
                                  int n, float* __restrict__ C) {
   const int64_t total = static_cast<int64_t>(n) * n;
@@ -1248,8 +1292,13 @@ extern "C" int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C,
     return CC_ERR_ARG;
   }
   const int64_t total = static_cast<int64_t>(n) * n;
-  int blocks = static_cast<int>(std::min<int64_t>((total + 255) / 256, 16384));
-  hipLaunchKernelGGL(consensus_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     M, I, n, C);
+  if (n % 4 == 0) {
+    const int blocks = std::min(n, 8192);  // 32 resident 256-thread workgroups per CU
+    hipLaunchKernelGGL(consensus_rows_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), M, I, n, C);
+  } else {
+    int blocks = static_cast<int>(std::min<int64_t>((total + 255) / 256, 16384));
+    hipLaunchKernelGGL(consensus_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       M, I, n, C);
+  }
   return launch_status("cc_consensus");
 }

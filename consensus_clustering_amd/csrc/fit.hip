@@ -226,7 +226,7 @@ extern "C" size_t cc_kmeans_fit_workspace_bytes(int n, int d, int m, int nh, con
     for (int k0 = 0; k0 < nK; k0 += 64) {
       const int nk = std::min(64, nK - k0);
       const int g = std::min(4 * P.cus, nh * nk);
-      engine = std::max(engine, cc_kmeans_f64_workspace_bytes(m, d, Ks + k0, nk, g));
+      engine = std::max(engine, cc_kmeans_f64_workspace_bytes(m, d, Ks + k0, nk, g, nh));
     }
   } else if (P.dpad <= 128) {
     if (P.nU <= 0) return 0;
@@ -306,8 +306,8 @@ extern "C" int cc_kmeans_fit(const void* X, int n, int d, const int32_t* idx_hm,
     for (int k0 = 0; k0 < nK; k0 += 64) {
       const int nk = std::min(64, nK - k0);
       int g = std::min(4 * P.cus, nh * nk);
-      while (g > 1 && off + align256(cc_kmeans_f64_workspace_bytes(m, d, Ks + k0, nk, g)) > ws_bytes) g /= 2;
-      const size_t eb = cc_kmeans_f64_workspace_bytes(m, d, Ks + k0, nk, g);
+      while (g > 1 && off + align256(cc_kmeans_f64_workspace_bytes(m, d, Ks + k0, nk, g, nh)) > ws_bytes) g /= 2;
+      const size_t eb = cc_kmeans_f64_workspace_bytes(m, d, Ks + k0, nk, g, nh);
       if (eb == 0 || off + eb > ws_bytes) {
         cc::set_error("cc_kmeans_fit: workspace too small");
         return CC_ERR_ARG;

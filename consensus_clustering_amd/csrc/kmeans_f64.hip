@@ -1427,12 +1427,16 @@ extern "C" int cc_kmeans_f64_stamps(unsigned long long* out) {
 }
 #endif
 
-extern "C" size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks, int nK, int grid) {
-  if (m <= 0 || d <= 0 || !Ks || nK <= 0 || grid <= 0) return 0;
+// A launch takes min(grid, nh) resamples (their per-resample slots) and runs them on the grid.
+static size_t f64_ws_bytes(const F64Layout& L, int grid, int nh) {
+  return WS_HEADER + L.per_wg * static_cast<size_t>(grid) + L.per_res * static_cast<size_t>(std::min(grid, nh));
+}
+
+extern "C" size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks, int nK, int grid, int nh) {
+  if (m <= 0 || d <= 0 || !Ks || nK <= 0 || grid <= 0 || nh <= 0) return 0;
   int kmax = 1;
   for (int i = 0; i < nK; ++i) kmax = std::max(kmax, Ks[i]);
-  const F64Layout L = f64_layout(m, d, kmax);
-  return WS_HEADER + (L.per_wg + L.per_res) * static_cast<size_t>(grid);
+  return f64_ws_bytes(f64_layout(m, d, kmax), grid, nh);
 }
 
 extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_hm, int H, int m,
@@ -1463,7 +1467,7 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
   const int nh = h_end - h_begin;
   if (nh == 0) return CC_OK;
   const F64Layout L = f64_layout(m, d, kmax);
-  if (!workspace || ws_bytes < WS_HEADER + (L.per_wg + L.per_res) * static_cast<size_t>(grid)) {
+  if (!workspace || ws_bytes < f64_ws_bytes(L, grid, nh)) {
     cc::set_error("cc_kmeans_f64: workspace too small");
     return CC_ERR_ARG;
   }

@@ -455,9 +455,11 @@ __device__ bool grid_sync(const GridWs& gw, unsigned& gen) {
     int ok = 1;
     const unsigned want = gen + 1;
     if constexpr (FULL) __threadfence();  // release (writes back this XCD's L2)
-    // arrival and generation: release / acquire at agent scope (the slice minima of the light form
-    // are agent-scope atomics; these order them against the arrival and the generation word)
-    if (__hip_atomic_fetch_add(&gw.bar[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+    // arrival and generation at agent scope (the slice minima of the light form are agent-scope
+    // atomics; these order them against the arrival and the generation word).  The arrival is
+    // acquire-release: the last arriver's fetch_add reads every earlier arrival (a release
+    // sequence on bar[0]), so its generation store below carries their writes to the waiters.
+    if (__hip_atomic_fetch_add(&gw.bar[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
       __hip_atomic_store(&gw.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_s_waitcnt(0x0F70);  // the reset is done before the release
       if constexpr (FULL) __threadfence();

@@ -160,6 +160,8 @@ def scatter_labels(idx_hm: torch.Tensor, labels_hm, n: int, out_nh: torch.Tensor
     if labels_hm is not None:
         assert labels_hm.dtype == torch.int32 and tuple(labels_hm.shape) == (H, m)
         labels_hm = labels_hm.contiguous()
+    if H == 0:  # a rank that owns no resample (dist.shard) has nothing to place
+        return
     base = out_nh[:, h_offset:]
     _lib.call("cc_scatter_labels", _lib.ptr(idx_hm), _lib.ptr(labels_hm), H, m, n,
               base.data_ptr(), ldl, stream_ptr())

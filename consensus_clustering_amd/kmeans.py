@@ -157,13 +157,15 @@ class BatchedKMeans:
     """All (h, K, init) k-means problems of a consensus fit, on one device."""
 
     def __init__(self, Ks, n_init=3, max_iter=300, tol=1e-4, random_state=0,
-                 workspace_budget=DEFAULT_WORKSPACE_BUDGET, seedmax=None, wide_budget=96 << 30):
+                 workspace_budget=None, seedmax=None, wide_budget=96 << 30):
         self.Ks = [int(k) for k in Ks]
         self.n_init = int(n_init)
         self.max_iter = int(max_iter)
         self.tol = float(tol)
         self.seed = int(random_state)
-        self.workspace_budget = int(workspace_budget)
+        # None: DEFAULT_WORKSPACE_BUDGET, which the float64 path may exceed to keep its grid at the
+        # kernel's occupancy; a budget the caller sets (any value) is never exceeded
+        self.workspace_budget = None if workspace_budget is None else int(workspace_budget)
         self.seedmax = None if seedmax is None else int(seedmax)
         self.wide_budget = int(wide_budget)
         self.stats = None
@@ -198,7 +200,7 @@ class BatchedKMeans:
         lib = _lib.load()
         per = lambda g: lib.cc_kmeans_workspace_bytes(m, Xd.shape[1], u_h.ctypes.data, nU, seedmax, g)
         grid = min(cus, nh * nU)
-        budget = min(self.workspace_budget, int(0.5 * torch.cuda.mem_get_info(dev)[0]))
+        budget = min(self.workspace_budget or DEFAULT_WORKSPACE_BUDGET, int(0.5 * torch.cuda.mem_get_info(dev)[0]))
         while grid > 1 and per(grid) > budget:
             grid //= 2
         ws = workspace(dev, per(grid))
@@ -230,19 +232,25 @@ class BatchedKMeans:
             Ks = self.Ks[k0:k0 + 64]
             Ks_np = np.ascontiguousarray(np.asarray(Ks, dtype=np.int32))
             g = int(grid or min(4 * cus, nh * len(Ks)))
-            per = lambda gg: lib.cc_kmeans_f64_workspace_bytes(m, d, Ks_np.ctypes.data, len(Ks), gg)
+            per = lambda gg: lib.cc_kmeans_f64_workspace_bytes(m, d, Ks_np.ctypes.data, len(Ks), gg, nh)
             # never more than half the free device memory.  At the DEFAULT budget the grid keeps two
             # resident workgroups per CU (the kernel's occupancy) even when their scratch exceeds
             # the budget: with one per CU the float64 fit runs ~1.25x longer
             # (profiles/r04/f64_budget_r4ak.txt).  A budget the caller set is never exceeded.
             free_half = int(0.5 * torch.cuda.mem_get_info(dev)[0])
-            if self.workspace_budget == DEFAULT_WORKSPACE_BUDGET:
-                cap = min(max(self.workspace_budget, per(min(g, 2 * cus))), free_half)
+            if self.workspace_budget is None:
+                cap = min(max(DEFAULT_WORKSPACE_BUDGET, per(min(g, 2 * cus))), free_half)
             else:
                 cap = min(self.workspace_budget, free_half)
-            if per(g) > cap:  # the largest grid that fits (the scratch is linear in the grid)
-                unit = per(2) - per(1)
-                g = max(1, min(g, int((cap - (per(1) - unit)) // unit)))
+            if per(g) > cap:  # the largest grid that fits (per(g) is non-decreasing in g)
+                lo, hi = 1, g
+                while lo < hi:
+                    mid = (lo + hi + 1) // 2
+                    if per(mid) <= cap:
+                        lo = mid
+                    else:
+                        hi = mid - 1
+                g = lo
             ws = workspace(dev, per(g))
             u, pos, stride = kpp_tables(Ks, self.n_init, self.seed, m, np.float64)
             u_d = torch.from_numpy(u).to(dev)

@@ -270,9 +270,10 @@ int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* xnorm, int 
  * the raw [n][d] float64 input (the kernel centres each resample by its own mean, as
  * KMeans.fit does).  Ks [nK] is a host array (nK <= 64); one persistent workgroup per
  * (resample, K) unit (or pair of K's); inertia is float64 here.  Workspace from
- * cc_kmeans_f64_workspace_bytes(m, d, Ks, nK, grid): grid workgroup areas and grid per-resample
- * slots (resamples beyond grid run in further launches on the same stream). */
-size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks, int nK, int grid);
+ * cc_kmeans_f64_workspace_bytes(m, d, Ks, nK, grid, nh): grid workgroup areas and min(grid, nh)
+ * per-resample slots for nh = h_end - h_begin (resamples beyond grid run in further launches on
+ * the same stream). */
+size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks, int nK, int grid, int nh);
 
 int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_hm, int H, int m, int h_begin,
                   int h_end, const int32_t* Ks, int nK, int n_init, int max_iter, double tol_rel,

@@ -3,7 +3,10 @@ as a W-rank torch.distributed job (gloo backend, every rank on cuda:0) and saves
 results.  It is started as a child process, so the ranks are spawned by a parent that has not
 touched the GPU.
 
-    python tests/dist_worker.py <fixture> <world> <keep 0|1> <out.npz> [backend]
+    python tests/dist_worker.py <fixture> <world> <keep 0|1> <out.npz> [backend] [H] [clusterer]
+
+H overrides the fixture's n_iterations (fewer resamples than ranks leaves a rank without any);
+clusterer 'gmm' runs the hybrid path (a host GaussianMixture per resample, tests/test_gpu_dist.py).
 
 backend 'nccl' (RCCL) needs one device per rank, so on a one-GPU box it runs with world 1 and
 CCMI_DIST_EXCHANGE_W1=1 (the exchange collectives then run on RCCL anyway).
@@ -24,7 +27,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank(rank, world, port, name, keep, out, backend="gloo"):
+def make_clusterer(kind):
+    if kind == "gmm":
+        from sklearn.mixture import GaussianMixture
+
+        return GaussianMixture(n_components=2)
+    return None
+
+
+def _rank(rank, world, port, name, keep, out, backend="gloo", H=0, clusterer=""):
     import torch
     import torch.distributed as dist
 
@@ -40,7 +51,9 @@ def _rank(rank, world, port, name, keep, out, backend="gloo"):
 
         f = load_fixture(name)
         meta = f["meta"]
-        cc = ConsensusClustering(K_range=[int(k) for k in f["K_range"]], n_iterations=meta["H"],
+        cc = ConsensusClustering(clusterer=make_clusterer(clusterer),
+                                 clusterer_options={} if clusterer else {'n_init': 3},
+                                 K_range=[int(k) for k in f["K_range"]], n_iterations=H or meta["H"],
                                  subsampling=meta["subsampling"], random_state=meta["random_state"],
                                  plot_cdf=False, keep_matrices=bool(keep))
         cc.fit(f["X"])
@@ -65,7 +78,9 @@ def main():
 
     name, world, keep, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     backend = sys.argv[5] if len(sys.argv) > 5 else "gloo"
-    mp.spawn(_rank, args=(world, _free_port(), name, keep, out, backend), nprocs=world, join=True)
+    H = int(sys.argv[6]) if len(sys.argv) > 6 else 0
+    clusterer = sys.argv[7] if len(sys.argv) > 7 else ""
+    mp.spawn(_rank, args=(world, _free_port(), name, keep, out, backend, H, clusterer), nprocs=world, join=True)
 
 
 if __name__ == "__main__":

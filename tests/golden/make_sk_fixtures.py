@@ -94,6 +94,21 @@ CASES = {
                     ref=[0, 1, 2]),
     "c4_full": dict(X=lambda: _expr(5_000, 20_000, 0), Ks=list(range(2, 13)), seed=0, classify=[0]),
 }
+def _f64_noisy(n, d, k):
+    """tests/test_gpu_kmeans.py::test_f64_labels_match_sklearn_float64's rows: blobs at seed n + d
+    (float32, then float64) plus N(0, 0.5^2) noise from default_rng(0)."""
+    X = _blobs(n, d, k, n + d).astype(np.float64)
+    X += np.random.default_rng(0).normal(scale=0.5, size=X.shape)
+    return X
+
+
+# tests/test_gpu_kmeans.py::test_f64_labels_match_sklearn_float64 (seed 3): sklearn float64 label
+# digests, n_iter and inertia of every (K, h)
+F64_SMALL = {
+    "f64_n29_d29": dict(X=lambda: _f64_noisy(29, 29, 3), Ks=[2, 3, 4, 5, 6, 7, 8, 9, 10], seed=3, H=6),
+    "f64_n600_d12": dict(X=lambda: _f64_noisy(600, 12, 4), Ks=[2, 3, 4, 6, 9], seed=3, H=4),
+    "f64_n300_d150": dict(X=lambda: _f64_noisy(300, 150, 3), Ks=[2, 3, 5], seed=3, H=3),
+}
 F64_CASE = dict(X=lambda: _blobs(50_000, 128, 8, 5, dtype=np.float64), Ks=list(range(2, 21)), seed=0, H=2)
 PAC_CASES = {
     # tests/test_gpu_parity_blobs.py: C2 shape at H = 50, C3 shape at H = 16
@@ -156,14 +171,25 @@ def _classify_task(args):
     reasons = 0
     for bit, _ in uniq:
         reasons |= bit
-    print(f"  {case} K={K} h={h}: reasons={reasons} variants={len(uniq)} ({time.time() - t0:.1f} s)", flush=True)
+    # sklearn's own spread: each variant's adjusted Rand index to ref32 and its relative partition
+    # inertia difference (tests/sk_parity.py bounds a neighbour by these)
+    from sklearn.metrics import adjusted_rand_score
+    from tests.sk_parity import partition_ss
+
+    ss_ref = partition_ss(rows, ref32.astype(np.int64), K)
+    for u in uniq:
+        lab = u[1].astype(np.int64)
+        u.append(float(adjusted_rand_score(ref32.astype(np.int64), lab)))
+        u.append(float((partition_ss(rows, lab, K) - ss_ref) / ss_ref))
+    print(f"  {case} K={K} h={h}: reasons={reasons} variants={len(uniq)} "
+          f"ari_min={min([u[2] for u in uniq], default=1.0):.4f} ({time.time() - t0:.1f} s)", flush=True)
     return case, K, h, ref32, reasons, uniq
 
 
 def _ref_task(args):
     case, K, h, dt = args
     X = _X[case]
-    spec = CASES.get(case) or PAC_CASES.get(case) or F64_CASE
+    spec = CASES.get(case) or PAC_CASES.get(case) or F64_SMALL.get(case) or F64_CASE
     rows = X[indices(X.shape[0], spec["seed"], h)]
     lab, nit, inert = _fit(rows.astype(dt), K, spec["seed"])
     return case, K, h, lab, nit, inert
@@ -223,17 +249,19 @@ def make_classify(case, ex):
     m = int(0.8 * X.shape[0])
     ref32 = np.zeros((len(Ks), len(hs), m), dtype=np.int8)
     reasons = np.zeros((len(Ks), len(hs)), dtype=np.int32)
-    var_dig, var_owner, var_bits = [], [], []
+    var_dig, var_owner, var_bits, var_ari, var_dss = [], [], [], [], []
     by = {}
     for (_, K, h, r32, rs, uniq) in res:
         k, c = Ks.index(K), hs.index(h)
         ref32[k, c] = r32
         reasons[k, c] = rs
         by[(K, h)] = r32
-        for bit, lab in uniq:
+        for bit, lab, ari, dss in uniq:
             var_dig.append(digest(lab))
             var_owner.append((k, c))
             var_bits.append(bit)
+            var_ari.append(ari)
+            var_dss.append(dss)
     ref_digest = np.full((len(Ks), max(1, len(rhs))), "", dtype="U64")
     for (_, K, h, lab, _, _) in refs:
         ref_digest[Ks.index(K), rhs.index(h)] = digest(lab)
@@ -250,29 +278,31 @@ def make_classify(case, ex):
                         var_digest=np.array(var_dig, dtype="U64"),
                         var_owner=np.array(var_owner, dtype=np.int32).reshape(-1, 2),
                         var_bits=np.array(var_bits, dtype=np.int32), ref_digest=ref_digest,
+                        var_ari=np.array(var_ari, dtype=np.float64), var_dss=np.array(var_dss, dtype=np.float64),
                         meta=np.array(json.dumps(meta)))
     print(f"{case}: {len(res)} classified, {len(refs)} identity-only, {len(var_dig)} variants, "
           f"sensitive {int((reasons > 0).sum())} ({time.time() - t0:.0f} s)", flush=True)
 
 
-def make_f64(ex):
-    spec = F64_CASE
-    X = _X["f64_c3shape"]
+def make_f64(ex, case="f64_c3shape"):
+    spec = F64_SMALL.get(case, F64_CASE)
+    X = _X[case]
     Ks, H = spec["Ks"], spec["H"]
     t0 = time.time()
-    res = list(ex.map(_ref_task, [("f64_c3shape", K, h, np.float64) for K in Ks for h in range(H)]))
+    res = list(ex.map(_ref_task, [(case, K, h, np.float64) for K in Ks for h in range(H)]))
     dig = np.full((len(Ks), H), "", dtype="U64")
     nit = np.zeros((len(Ks), H), dtype=np.int32)
     inert = np.zeros((len(Ks), H), dtype=np.float64)
     for (_, K, h, lab, it, ine) in res:
         k = Ks.index(K)
         dig[k, h], nit[k, h], inert[k, h] = digest(lab), it, ine
-    meta = dict(kind="f64", case="f64_c3shape", n=X.shape[0], d=X.shape[1], Ks=Ks, seed=spec["seed"], frac=0.8,
-                H=H, x_sha256=digest(X), note="make_blobs(50000, 128, 8 centers, std 1, box (-10, 10), seed 5) "
-                "float64; sklearn KMeans(n_init=3) float64, 1 thread")
-    np.savez_compressed(os.path.join(OUT, "f64_c3shape.npz"), digest64=dig, n_iter=nit, inertia=inert,
+    note = ("make_blobs(50000, 128, 8 centers, std 1, box (-10, 10), seed 5) float64"
+            if case == "f64_c3shape" else "tests/test_gpu_kmeans.py blobs + N(0, 0.5^2) noise")
+    meta = dict(kind="f64", case=case, n=X.shape[0], d=X.shape[1], Ks=Ks, seed=spec["seed"], frac=0.8,
+                H=H, x_sha256=digest(X), note=note + "; sklearn KMeans(n_init=3) float64, 1 thread")
+    np.savez_compressed(os.path.join(OUT, f"{case}.npz"), digest64=dig, n_iter=nit, inertia=inert,
                         meta=np.array(json.dumps(meta)))
-    print(f"f64_c3shape: {len(res)} fits ({time.time() - t0:.0f} s); n_iter {nit.min()}..{nit.max()}", flush=True)
+    print(f"{case}: {len(res)} fits ({time.time() - t0:.0f} s); n_iter {nit.min()}..{nit.max()}", flush=True)
 
 
 def make_pac(case, ex):
@@ -306,9 +336,10 @@ def make_pac(case, ex):
 
 def main(argv):
     os.makedirs(OUT, exist_ok=True)
-    want = argv or list(CASES) + ["f64_c3shape"] + list(PAC_CASES)
+    want = argv or list(CASES) + ["f64_c3shape"] + list(F64_SMALL) + list(PAC_CASES)
     for c in want:
-        spec = CASES.get(c) or PAC_CASES.get(c) or (F64_CASE if c == "f64_c3shape" else None)
+        spec = (CASES.get(c) or PAC_CASES.get(c) or F64_SMALL.get(c)
+                or (F64_CASE if c == "f64_c3shape" else None))
         assert spec is not None, c
         _X[c] = spec["X"]()
     workers = int(os.environ.get("SK_WORKERS", "8"))
@@ -319,7 +350,7 @@ def main(argv):
             elif c in PAC_CASES:
                 make_pac(c, ex)
             else:
-                make_f64(ex)
+                make_f64(ex, c)
 
 
 if __name__ == "__main__":

@@ -125,8 +125,12 @@ def kmeans_at_engine_precision(rows, K, seed, n_init=3, s=4, max_iter=300, tol=1
 # reason bits of tests/golden/make_sk_fixtures.py
 REASONS = {1: "f32!=f64", 2: "nudge", 4: "threads", 8: "alignment", 16: "engine-precision"}
 # a rounding-sensitive problem whose engine labels match none of sklearn's own variants must still
-# be a neighbouring optimum of sklearn's: adjusted Rand index and partition inertia bounds
-NEIGHBOUR_MIN_ARI = 0.6
+# be a neighbouring optimum of sklearn's: its adjusted Rand index to sklearn's float32 labels must
+# reach NEIGHBOUR_MIN_ARI, or, where sklearn's own rounding variants of that problem (its float64
+# fit, the 2^-22 nudges, ...) land farther from its float32 labels than that, the lowest ARI among
+# those variants (the fixture's var_ari): the engine may differ from sklearn's float32 fit by as
+# much as sklearn differs from itself, and no more.  The partition inertia bound is absolute.
+NEIGHBOUR_MIN_ARI = 0.95
 NEIGHBOUR_MAX_DSS = 2e-4   # |SS(engine) - SS(sklearn)| / SS(sklearn), SS in float64
 
 
@@ -198,7 +202,7 @@ def sklearn_identical(case, X, labels, idx, max_K=None):
     return checked
 
 
-def sklearn_parity(case, X, labels, idx, max_unexplained=0, Ks=None):
+def sklearn_parity(case, X, labels, idx, max_unexplained=0, Ks=None, known=()):
     """The engine's labels of every (K, h) the fixture classifies against sklearn's float32 KMeans
     on the same rows (tests/golden/make_sk_fixtures.py, generated once in the development
     container on one thread, so the verdict does not depend on the GPU box's CPU BLAS).
@@ -209,10 +213,11 @@ def sklearn_parity(case, X, labels, idx, max_unexplained=0, Ks=None):
         perturbations (its float64 fit, a 2^-22 nudge of the inputs, 8 threads, another buffer
         alignment, or its own algorithm at the engine's operand precision);
       * a neighbour: sklearn's fit is rounding-sensitive there (some perturbation moved it), and
-        the engine's partition is within NEIGHBOUR_MAX_DSS relative partition inertia and
-        NEIGHBOUR_MIN_ARI adjusted Rand index of sklearn's (both reported);
-      * unexplained otherwise.  At most `max_unexplained` may be (0 unless a caller documents a
-        known gap).
+        the engine's partition is within NEIGHBOUR_MAX_DSS relative partition inertia of sklearn's
+        and its adjusted Rand index to sklearn's labels is at least min(NEIGHBOUR_MIN_ARI, the
+        lowest ARI of sklearn's own variants of that problem) (reported with the bound);
+      * unexplained otherwise.  Only the (K, h) problems a caller lists in `known` (documented
+        gaps) may be unexplained, at most `max_unexplained` of them.
     Prints and returns (identical, explained, total)."""
     from sklearn.metrics import adjusted_rand_score
 
@@ -246,14 +251,18 @@ def sklearn_parity(case, X, labels, idx, max_unexplained=0, Ks=None):
             ari = adjusted_rand_score(ref, got)
             rec = (K, h, round(float(np.mean(got == ref)), 5), round(ari, 4), float(f"{dss:.2e}"))
             reasons = int(f["reasons"][k, c])
-            if reasons and ari >= NEIGHBOUR_MIN_ARI and abs(dss) <= NEIGHBOUR_MAX_DSS:
+            spread = [float(f["var_ari"][v]) for v in owner.get((k, c), [])] if "var_ari" in f else []
+            ari_min = min([NEIGHBOUR_MIN_ARI] + spread)
+            rec = rec + (round(ari_min, 4),)
+            if reasons and ari >= ari_min and abs(dss) <= NEIGHBOUR_MAX_DSS:
                 neighbours.append(rec + ("+".join(n for b, n in REASONS.items() if reasons & b),))
             else:
                 unexplained.append(rec + (reasons,))
     total = len(fKs) * len(hs)
     explained = len(variants) + len(neighbours)
     print(f"sklearn parity [{case}]: {same}/{total} identical; {len(variants)} equal to a sklearn variant "
-          f"{variants}; {len(neighbours)} rounding-sensitive neighbours (K, h, equal, ARI, dSS, why) "
+          f"{variants}; {len(neighbours)} rounding-sensitive neighbours (K, h, equal, ARI, dSS, ARI bound, why) "
           f"{neighbours}; {len(unexplained)} unexplained {unexplained}")
     assert len(unexplained) <= max_unexplained, unexplained
+    assert all((u[0], u[1]) in set(map(tuple, known)) for u in unexplained), (unexplained, known)
     return same, explained, total

@@ -149,10 +149,10 @@ def test_tile_range_sharding_is_exact():
     np.testing.assert_array_equal(c1, c3)
 
 
-def test_consensus_matrix_kernel():
+@pytest.mark.parametrize("n", [333, 2052])  # the flat kernel (n % 4 != 0) and the row kernel
+def test_consensus_matrix_kernel(n):
     dev = engine.require_gpu()
     rng = np.random.default_rng(0)
-    n = 333
     I = rng.integers(0, 1001, size=(n, n)).astype(np.int32)
     I = np.maximum(I, I.T)
     M = (I * rng.random((n, n))).astype(np.int32)

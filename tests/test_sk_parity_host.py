@@ -54,4 +54,6 @@ def test_sk_fixture_classifier_on_its_own_labels():
     bad[k][0] = lab
     with pytest.raises(AssertionError):
         sklearn_parity(case, X, bad, idx, Ks=Ks)
-    sklearn_parity(case, X, bad, idx, Ks=Ks, max_unexplained=1)
+    with pytest.raises(AssertionError):  # unexplained but not listed as a known gap
+        sklearn_parity(case, X, bad, idx, Ks=Ks, max_unexplained=1)
+    sklearn_parity(case, X, bad, idx, Ks=Ks, max_unexplained=1, known=[(Ks[k], 0)])
