@@ -93,6 +93,8 @@ CASES = {
     "c2_full": dict(X=lambda: _blobs(10_000, 64, 6, 0), Ks=list(range(2, 16)), seed=0, classify=[3, 4],
                     ref=[0, 1, 2]),
     "c4_full": dict(X=lambda: _expr(5_000, 20_000, 0), Ks=list(range(2, 13)), seed=0, classify=[0]),
+    # C5 (n = 200 000, m = 160 000, d = 32, K = 2..10): the d = 32 pair-mode engine at its real m
+    "c5_full": dict(X=lambda: _blobs(200_000, 32, 6, 0), Ks=list(range(2, 11)), seed=0, classify=[0, 1]),
 }
 def _f64_noisy(n, d, k):
     """tests/test_gpu_kmeans.py::test_f64_labels_match_sklearn_float64's rows: blobs at seed n + d

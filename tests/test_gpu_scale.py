@@ -9,7 +9,7 @@ For each config the drop-in fit runs at the real n, d, K range and H, then:
     ragged last column block; diagonal tiles) is recomputed on the host from the fit's own
     labels: the co-sampling tile (diagonal = per-row sample counts) and the 20 histogram
     counts of every K must be bit-identical to the GPU's (CC.py:264, :287-290, :338-344);
-  * C2 / C3: the k-means labels of the first resamples at the full m equal sklearn's
+  * C2 / C3 / C5: the k-means labels of the first resamples at the full m equal sklearn's
     KMeans (the reference's clusterer, CC.py:282) for every K <= the true number of blobs, and
     for further resamples over the WHOLE K range every disagreement with sklearn's float32
     fit is a problem where sklearn's own float32 and float64 fits disagree (sk_parity);
@@ -183,10 +183,16 @@ def test_c3_full_size():
 
 
 def test_c5_full_size():
+    """BASELINE config 5 (n = 200k, d = 32, K = 2..10, H = 256) at full size: pair-count sums,
+    label columns, oracle-checked tiles, and the d = 32 pair-mode k-means at its real m = 160 000
+    against sklearn's float32 fits of resamples 0 and 1 (tests/golden/sk/c5_full.npz): identical
+    for K <= k_true = 6, classified above."""
     cfg, X, cc = fit_config("c5")
     check_counts_sum(cfg, cc)
     check_labels(cfg, cc)
     check_tiles(cfg, cc, Ks_check=[2, 6, 10])
+    check_kmeans("c5_full", cfg, X, cc)
+    sklearn_parity("c5_full", X, cc.labels_, cc.resampling_indices_, Ks=cfg["Ks"])
 
 
 def test_c2_full_size_with_matrices():
