@@ -377,8 +377,13 @@ __device__ __forceinline__ void build_afrag(double* dst, Row row, int nrow, int 
 // centres at rows off_a .. off_a + K_a; no per-problem padding to 16 rows), each pass of 16 CT
 // rows feeds every problem's own running (distance, label) per row (jm[J] = a << 8 | j, gof[a]:
 // the problem of slot a), and a row tile's B operands are read once for all of them.
+// The passes over the rows (estep_packed, msum_packed, kpp_mfma_multi, kpp_search_multi,
+// kpp_pots_multi) are out of line (round 6): each gets its own register allocation instead of
+// sharing the kernel body's, whose VGPR spills fell from 91 / 162 to 51 / 64 (GM = 4 / 6); a call
+// per pass costs nothing measurable.  C2 H = 500 1.08x, C5 H = 64 1.15x, C3 H = 128 0.99x, results
+// identical (profiles/r06/f64_noinline_ab.txt).
 template <int RT, int CT, int NA>
-__device__ void estep_packed(const WG& w, int na, const int* gof, const int* jm, const double* cnp, int nJ, int d,
+__device__ __attribute__((noinline)) void estep_packed(const WG& w, int na, const int* gof, const int* jm, const double* cnp, int nJ, int d,
                              int m, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int ntile = (m + 15) >> 4;
@@ -498,7 +503,7 @@ __device__ __forceinline__ int estep_multi(const WG& w, unsigned act, unsigned p
 // g << 8 | t, the candidate row cand[g * TMAX + t]; first centre: one column per problem), all
 // nc <= GMAX * TMAX of them as the centres of one pass over the rows; each value is kpp_mfma's
 // ((-2 x.c) + |c|^2) + |x|^2 clipped at 0, min with problem g's closest.
-__device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const int* cand, const int* col, int nc,
+__device__ __attribute__((noinline)) void kpp_mfma_multi(const WG& w, int d, int m, const int* cand, const int* col, int nc,
                                                bool first, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int ntile = (m + 15) >> 4;
@@ -560,7 +565,7 @@ __device__ __forceinline__ void kpp_mfma_multi(const WG& w, int d, int m, const 
 // problems; lane l's A operand reads the labels of its own cluster's problem), and the B operands
 // (the rows) are loaded once per k-step for all of them.
 template <int CTP, int FTP>
-__device__ void msum_packed(const WG& w, unsigned par, const int* gof, const int* jm, int nJ, int d, int m, int tid) {
+__device__ __attribute__((noinline)) void msum_packed(const WG& w, unsigned par, const int* gof, const int* jm, int nJ, int d, int m, int tid) {
   const int l = tid & 63, q = l >> 4, c16 = l & 15;
   const int nct = (nJ + 15) >> 4, nft = (d + 15) >> 4;
   const int nfg = (nft + FTP - 1) / FTP;
@@ -675,7 +680,7 @@ __device__ __forceinline__ int walker_slot(int tid) {
 // cumulative sum in row order, 8 partial sums then one comparison with the next of the sorted
 // thresholds (the sums do not decrease, so the thresholds are crossed in order).
 constexpr int CBM = 512;
-__device__ void kpp_search_multi(const F64Args& a, const WG& w, const GroupInfo& gi, const int* sg, int ns, int c,
+__device__ __attribute__((noinline)) void kpp_search_multi(const F64Args& a, const WG& w, const GroupInfo& gi, const int* sg, int ns, int c,
                                  const double* pot, int* cand, double* sb, int* sflag, double* s_thr, int* s_tix,
                                  int tid) {
   const int m = w.m;
@@ -773,7 +778,7 @@ __device__ __forceinline__ double chain_sum(const double* x, int i0, int e, int 
 // The candidates' potentials for every column of a lockstep group at once (col[c] = g << 8 | t):
 // pot[g TMAX + t] = blas_gemv_t_ones(column t of w.dc_of(g), m, t, ntr_g), its (column,
 // 2048-row block, lane) accumulator chains one per thread, the folds by thread c.
-__device__ void kpp_pots_multi(const WG& w, const int* ntrg, const int* col, int nc, double* part, double* pot,
+__device__ __attribute__((noinline)) void kpp_pots_multi(const WG& w, const int* ntrg, const int* col, int nc, double* part, double* pot,
                                int tid) {
   const int m = w.m;
   const int m1 = m & ~3;

@@ -15,10 +15,14 @@ Three kinds of fixture under tests/golden/sk/:
 * ``<case>.npz`` (kind "classify"): for the problems a test checks with tests/sk_parity.py,
   sklearn's float32 labels (``ref32``), and for each problem the rounding-sensitivity evidence
   sklearn itself gives: its float64 fit, eight 2^-22 nudges of the inputs, the same fit on 8
-  threads and on copies at four buffer alignments, and sklearn's algorithm at the engine's
-  operand precision (sk_parity.kmeans_at_engine_precision, scale exponents 4 and 7).  Each
-  perturbation whose labels differ from ref32 sets a reason bit and its labels are kept as a
-  "variant" (its digest: the tests compare variants for identity only).  Problems checked for
+  threads and on copies at four buffer alignments, sklearn's algorithm at the engine's operand
+  precision (sk_parity.kmeans_at_engine_precision, scale exponents 4 and 7; for 64 < d <= 128
+  also with the d = 128 engine's sparse M-step), and sklearn's fit opened up
+  (sk_parity.sklearn_inits: the same Cython Lloyd step by step): its other inits whose
+  partition inertia is within NEIGHBOUR_MAX_DSS of the chosen one's, and the near-tie
+  assignments along every init's float32 trajectory.  Each perturbation whose labels differ
+  from ref32 sets a reason bit and its labels are kept as a "variant" (digest, labels, ARI and
+  relative partition inertia to ref32); a near tie sets its own bit.  Problems checked for
   identity only store a label digest.
 * ``f64_c3shape.npz`` (kind "f64"): sklearn float64 label digests, n_iter and inertia at the C3
   shape (n = 50 000, m = 40 000, d = 128, K = 2..20, 2 resamples) for cc_kmeans_f64.
@@ -49,7 +53,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, HERE)
 
 # reason bits (tests/sk_parity.py reads the same values)
-F32_F64, NUDGE, THREADS, ALIGN, ENGINE = 1, 2, 4, 8, 16
+F32_F64, NUDGE, THREADS, ALIGN, ENGINE, ENGINE_SPARSE, NEAR_TIE, OTHER_INIT = 1, 2, 4, 8, 16, 32, 64, 128
 NUDGE_DRAWS = 8  # random-sign 2^-22 relative nudges of the inputs per problem
 
 
@@ -161,6 +165,24 @@ def _classify_task(args):
     with threadpool_limits(1):
         for sx in (4, 7):
             note(ENGINE, kmeans_at_engine_precision(rows, K, seed, 3, s=sx).astype(np.int8))
+        if 64 < rows.shape[1] <= 128:  # the d = 128 engine's sparse M-step (kmeans.hip kSparse)
+            for sx in (4, 7):
+                note(ENGINE_SPARSE, kmeans_at_engine_precision(rows, K, seed, 3, s=sx, sparse=True).astype(np.int8))
+    # sklearn's fit opened up (tests/sk_parity.py sklearn_inits): its per-init results and the
+    # near-tie assignments along each init's float32 trajectory.  A near tie (a row whose two
+    # nearest centres are closer than float32's distance error) is a rounding-decided label
+    # of sklearn's own run; another init whose fixed point is within NEIGHBOUR_MAX_DSS of the
+    # chosen one's partition inertia is the labelling best-of-n_init picks when that rounding
+    # moves the chosen init's fixed point.
+    from tests.sk_parity import NEIGHBOUR_MAX_DSS, partition_ss, sklearn_inits
+
+    init_labels, _, ties, best = sklearn_inits(rows, K, seed)
+    assert np.array_equal(best, ref32), (case, K, h, "opened-up sklearn != KMeans.fit")
+    near_tie = int(ties.sum())
+    ss0 = partition_ss(rows, ref32.astype(np.int64), K)
+    for lab in init_labels:
+        if abs(partition_ss(rows, lab.astype(np.int64), K) - ss0) <= NEIGHBOUR_MAX_DSS * ss0:
+            note(OTHER_INIT, lab)
     # unique variants, reason bits OR-ed
     uniq = []
     for bit, lab in variants:
@@ -170,7 +192,7 @@ def _classify_task(args):
                 break
         else:
             uniq.append([bit, lab])
-    reasons = 0
+    reasons = NEAR_TIE if near_tie else 0
     for bit, _ in uniq:
         reasons |= bit
     # sklearn's own spread: each variant's adjusted Rand index to ref32 and its relative partition
@@ -183,7 +205,7 @@ def _classify_task(args):
         lab = u[1].astype(np.int64)
         u.append(float(adjusted_rand_score(ref32.astype(np.int64), lab)))
         u.append(float((partition_ss(rows, lab, K) - ss_ref) / ss_ref))
-    print(f"  {case} K={K} h={h}: reasons={reasons} variants={len(uniq)} "
+    print(f"  {case} K={K} h={h}: reasons={reasons} variants={len(uniq)} near_ties={near_tie} "
           f"ari_min={min([u[2] for u in uniq], default=1.0):.4f} ({time.time() - t0:.1f} s)", flush=True)
     return case, K, h, ref32, reasons, uniq
 
@@ -251,7 +273,7 @@ def make_classify(case, ex):
     m = int(0.8 * X.shape[0])
     ref32 = np.zeros((len(Ks), len(hs), m), dtype=np.int8)
     reasons = np.zeros((len(Ks), len(hs)), dtype=np.int32)
-    var_dig, var_owner, var_bits, var_ari, var_dss = [], [], [], [], []
+    var_dig, var_owner, var_bits, var_ari, var_dss, var_lab = [], [], [], [], [], []
     by = {}
     for (_, K, h, r32, rs, uniq) in res:
         k, c = Ks.index(K), hs.index(h)
@@ -264,6 +286,7 @@ def make_classify(case, ex):
             var_bits.append(bit)
             var_ari.append(ari)
             var_dss.append(dss)
+            var_lab.append(np.asarray(lab, dtype=np.int8))
     ref_digest = np.full((len(Ks), max(1, len(rhs))), "", dtype="U64")
     for (_, K, h, lab, _, _) in refs:
         ref_digest[Ks.index(K), rhs.index(h)] = digest(lab)
@@ -275,12 +298,14 @@ def make_classify(case, ex):
     meta = dict(kind="classify", case=case, n=X.shape[0], d=X.shape[1], Ks=Ks, seed=spec["seed"], frac=0.8,
                 classify=hs, ref=rhs, x_sha256=digest(X), sklearn=sklearn.__version__, numpy=np.__version__,
                 threads=1, nudge_draws=NUDGE_DRAWS, reason_bits=dict(f32_f64=F32_F64, nudge=NUDGE, threads=THREADS, align=ALIGN,
-                                            engine=ENGINE))
+                                            engine=ENGINE, engine_sparse=ENGINE_SPARSE, near_tie=NEAR_TIE,
+                                            other_init=OTHER_INIT))
     np.savez_compressed(os.path.join(OUT, f"{case}.npz"), ref32=ref32, reasons=reasons,
                         var_digest=np.array(var_dig, dtype="U64"),
                         var_owner=np.array(var_owner, dtype=np.int32).reshape(-1, 2),
                         var_bits=np.array(var_bits, dtype=np.int32), ref_digest=ref_digest,
                         var_ari=np.array(var_ari, dtype=np.float64), var_dss=np.array(var_dss, dtype=np.float64),
+                        var_labels=(np.stack(var_lab) if var_lab else np.zeros((0, m), dtype=np.int8)),
                         meta=np.array(json.dumps(meta)))
     print(f"{case}: {len(res)} classified, {len(refs)} identity-only, {len(var_dig)} variants, "
           f"sensitive {int((reasons > 0).sum())} ({time.time() - t0:.0f} s)", flush=True)
