@@ -180,7 +180,11 @@ def _classify_task(args):
     assert np.array_equal(best, ref32), (case, K, h, "opened-up sklearn != KMeans.fit")
     near_tie = int(ties.sum())
     ss0 = partition_ss(rows, ref32.astype(np.int64), K)
+    from sklearn.cluster._k_means_common import _is_same_clustering
+
     for lab in init_labels:
+        if _is_same_clustering(lab.astype(np.int32), ref32.astype(np.int32), K):
+            continue  # the chosen partition itself (labels permuted): no new evidence
         if abs(partition_ss(rows, lab.astype(np.int64), K) - ss0) <= NEIGHBOUR_MAX_DSS * ss0:
             note(OTHER_INIT, lab)
     # unique variants, reason bits OR-ed

@@ -223,7 +223,10 @@ REASONS = {1: "f32!=f64", 2: "nudge", 4: "threads", 8: "alignment", 16: "engine-
 # fixture's var_labels), its radius the lowest adjusted Rand index of a variant to the float32
 # labels (var_ari), capped at NEIGHBOUR_MIN_ARI.  The engine's labels must reach that ARI to the
 # NEAREST member of the cloud: they may differ from sklearn by as much as sklearn's own rounding
-# moves it, and no more.  The partition inertia bound is absolute.
+# moves it, and no more.  The cloud also holds sklearn's other inits whose partition inertia is
+# within NEIGHBOUR_MAX_DSS of the chosen one's (best-of-n_init picks one of them when rounding moves
+# the chosen init's fixed point); they do not widen the radius.  The partition inertia bound is
+# absolute.
 NEIGHBOUR_MIN_ARI = 0.95
 NEIGHBOUR_MAX_DSS = 2e-4   # |SS(engine) - SS(sklearn)| / SS(sklearn), SS in float64
 
@@ -347,7 +350,10 @@ def sklearn_parity(case, X, labels, idx, max_unexplained=0, Ks=None, known=()):
             rec = (K, h, round(float(np.mean(got == ref)), 5), round(ari, 4), float(f"{dss:.2e}"))
             reasons = int(f["reasons"][k, c])
             vs = owner.get((k, c), [])
-            spread = [float(f["var_ari"][v]) for v in vs] if "var_ari" in f else []
+            # the radius comes from the rounding perturbations only: another init (bit 128) is a
+            # member of the cloud, not a measure of how far rounding moves sklearn's result
+            spread = ([float(f["var_ari"][v]) for v in vs if int(f["var_bits"][v]) & ~128]
+                      if "var_ari" in f else [])
             ari_min = min([NEIGHBOUR_MIN_ARI] + spread)
             near = max([ari] + ([adjusted_rand_score(f["var_labels"][v].astype(np.int64), got) for v in vs]
                                 if "var_labels" in f else []))

@@ -14,9 +14,11 @@ import os
 import sys
 
 root, config, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+# tiles_kernel<1, false> is the co-sampling instantiation (demangled names carry every template
+# argument)
 KERNELS = {"cc_kmeans_batched": lambda k: "kmeans_kernel" in k,
-           "cc_coassoc": lambda k: "tiles_kernel" in k and "<1>" not in k,
-           "cc_cosample": lambda k: "tiles_kernel<1>" in k}
+           "cc_coassoc": lambda k: "tiles_kernel" in k and "tiles_kernel<1," not in k,
+           "cc_cosample": lambda k: "tiles_kernel<1," in k}
 tot = collections.defaultdict(float)
 disp = collections.defaultdict(set)
 for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
