@@ -190,7 +190,7 @@ def consensus_roofline(dev, n, H, reps=5):
     g = torch.Generator(device=dev)
     g.manual_seed(0)
     I = torch.randint(H // 2, H + 1, (n, n), dtype=torch.int32, device=dev, generator=g)
-    M = (I.to(torch.float32) * torch.rand((n, n), device=dev, generator=g)).to(torch.int32)
+    M = torch.randint(0, H // 2 + 1, (n, n), dtype=torch.int32, device=dev, generator=g)  # M <= I
     engine.consensus(M, I)  # warm-up (and the allocation of C)
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]

@@ -1,6 +1,7 @@
 # Parameterised GPU run (from the repo root on the box, through gpurun):
 #   TAG=name               output directory gpurun_out/$TAG
-#   TESTS="sel..."         pytest selection run with -m gpu (files and/or -k ...); unset: no tests
+#   TESTS="sel..."         pytest files/node ids run with -m gpu; unset: no tests
+#   KEXPR="expr"           pytest -k expression
 #   BENCH="c3 c2 ..."      bench.py configs, one JSON line each (BENCH_ARGS: extra arguments)
 #   PROF=1                 rocprofv3 kernel-trace summary of `bench.py --steps 2` at the first BENCH config
 # Every GPU step has its own time limit; the script stops at the first failure.
@@ -10,7 +11,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-run}
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 if [ -n "$TESTS" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest $TESTS -m gpu -v -s --timeout 300 --timeout-method thread -x > $OUT/tests.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest $TESTS ${KEXPR:+-k "$KEXPR"} -m gpu -v -s --timeout 300 --timeout-method thread -x > $OUT/tests.log 2>&1
   rc=$?
   echo "TESTS rc=$rc passed=$(grep -c ' PASSED' $OUT/tests.log)"; grep -E "FAILED|Error|error" $OUT/tests.log | head -8
   [ $rc -eq 0 ] || exit $rc
