@@ -301,8 +301,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # CCMI_BENCH_BACKEND=gloo (tests only): every rank on device LOCAL_RANK mod the device count
+        # over gloo, to exercise this multi-rank path on a one-GPU box, where RCCL refuses two ranks
+        # on one device; the driver's N-GPU runs use RCCL ("nccl"), one rank per GPU
+        backend = os.environ.get("CCMI_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            tdist.init_process_group(backend)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from consensus_clustering_amd import ConsensusClustering, engine
