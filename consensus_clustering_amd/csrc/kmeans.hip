@@ -76,8 +76,9 @@ constexpr int NLS = 8;              // E-step Lloyd steps per E/M wave (one Lloy
 constexpr int NSS = 8;              // E-step seeding steps per E/M wave (two seeding items each)
 constexpr int NLS_D = 3;            // ... per distance wave (they take a share of the E-steps;
 constexpr int NSS_D = 2;            //     more spill their A fragments at d = 128)
-constexpr int IMAX = 64;            // work items per sweep
+constexpr int IMAX = 128;           // work items per sweep (80 seeding candidates + 44 Lloyd steps fit)
 constexpr int PMAX = CC_KM_PMAX;    // problems per unit
+constexpr int LSN = PMAX;           // label hand-off rows per buffer (indexed by problem)
 constexpr int TMAX = 6;             // max local trials: 2 + floor(ln 127)
 constexpr int KMAX = 127;
 constexpr int DSD = CW + 4;         // distance-tile row stride (floats): 16-B rows, conflict-free b128
@@ -232,8 +233,8 @@ struct Lay {
   static constexpr int U_END = OFF_D + 2 * DBUF;
   static constexpr int S_BYTES = CW * DP * 4;  // centre sums [CW][DP] f32, aliasing ring + D
   static_assert(S_BYTES <= U_END, "centre sums must fit in the ring + distance tiles");
-  static constexpr int OFF_LS = (U_END + 32 + 15) / 16 * 16;  // labels [2][IMAX][RT] u8 (32 B slack: E-step over-reads)
-  static constexpr int OFF_XN = OFF_LS + kLsb<DP> * IMAX * RT;  // row norms [kRing][64] f32 (DMA'd, 32 used)
+  static constexpr int OFF_LS = (U_END + 32 + 15) / 16 * 16;  // labels [2][LSN][RT] u8 (32 B slack: E-step over-reads)
+  static constexpr int OFF_XN = OFF_LS + kLsb<DP> * LSN * RT;  // row norms [kRing][64] f32 (DMA'd, 32 used)
   static constexpr int OFF_ST = OFF_XN + kRing<DP> * 64 * 4;
   static constexpr int TOTAL = OFF_ST + ((sizeof(State) + 15) / 16) * 16;
   static_assert(TOTAL <= 163840, "LDS budget");
@@ -868,7 +869,7 @@ __device__ __forceinline__ void estep(const KArgs& a, const State& S, int t, int
   // labels in buffer te & 3
   const int coff = PM ? 128 * (te & 1) : 0;
   const float* drow = Dt + (PM ? ((te >> 1) & 1) : (te & 1)) * (RT * DSD) + ler * DSD;
-  uint8_t* lsb = Ls + (PM ? (te & 3) : (te & 1)) * (IMAX * RT);
+  uint8_t* lsb = Ls + (PM ? (te & 3) : (te & 1)) * (LSN * RT);
   const float xnr = XN[(te % kRing<DP>) * 64 + ler];
   constexpr float INF = __builtin_huge_valf();
   // seeding steps first (one item per half-wave): descriptors and distances of every step in
@@ -1616,7 +1617,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
           if (t >= 2) {
             const int tm = t - 2;
             const char* xs = ring + (tm % kRing<DP>) * LY::SLOT;
-            const uint8_t* lsb = Ls + (tm & 1) * (IMAX * RT);
+            const uint8_t* lsb = Ls + (tm & 1) * (LSN * RT);
             if (mact0 || mact1)  // both tiles share the transposed X reads (a tile without running
                                  // centres has an all-zero one-hot)
               mstep_tiles<DP, 2>(xs, lsb + myit0 * RT, lsb + myit1 * RT, lane, mycl0, mycl1, sacc0, sacc1, mcnt0, mcnt1, mact1);
@@ -1654,7 +1655,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_kernel(KArgs a) {
               const int tm = tA - 4 + g;
               if (tm >= 0 && tm < T && (mact0 || mact1)) {
                 const char* xs = ring + (tm % kRing<DP>) * LY::SLOT;
-                const uint8_t* lsb = Ls + (tm & 3) * (IMAX * RT);
+                const uint8_t* lsb = Ls + (tm & 3) * (LSN * RT);
                 mstep_tiles<DP, 2>(xs, lsb + myit0 * RT, lsb + myit1 * RT, lane, mycl0, mycl1, sacc0, sacc1, mcnt0, mcnt1, mact1);
               }
             }
