@@ -209,32 +209,42 @@ __device__ __forceinline__ void dma_wait_n() {
 }
 
 // ============================================================================================
-// E: distances of a 128-row tile to a 256-slot column tile, then the E-step.
-// Waves: 4 slot groups (64 slots) x 2 row groups (64 rows); per 32-feature stage each wave does
-// 2 k-steps x (2 x 2 blocks) x 3 MFMAs from register-staged, double-buffered LDS images.
+// E: distances of a 256-row tile to a 256-slot column tile, then the E-step.
+// Waves: 4 slot groups (64 slots) x 2 row groups (128 rows); per 32-feature stage each wave does
+// 2 k-steps x (2 x 4 blocks) x 3 MFMAs from register-staged LDS images: 0.5 fragment reads per
+// MFMA (the 128-row form read 0.67, and its LDS traffic per stage was about its MFMA time).  Every
+// output's MFMA chain (stage and k-step order, xh.cl then xl.ch then xh.ch) is the 128-row form's,
+// so the distances are bit-identical.  The E-step runs per 64-row quarter of the tile (the distance
+// tile of a quarter fits in the operand ring); a quarter's per-item sums are the wave sums of the
+// 128-row form's waves, and each 128-row half writes its own partial (part[.][2 rt + half]), so
+// the potentials and inertias keep their order too.
 // ============================================================================================
+constexpr int ER2 = 2 * ER;  // rows per E workgroup
 __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
-  // ring of 3 stages; a stage = A (slots) hi/lo planes + B (rows) hi/lo planes, 64-B rows
+  // ring of 2 stages; a stage = A (slots) hi/lo planes + B (rows) hi/lo planes, 64-B rows
   // (32 features) with the 16-B chunks XOR-swizzled by (row >> 2) & 3: conflict-free b128
   // fragment reads, and lane-linear 1-KiB pieces (16 rows of a plane) for the LDS-DMA fill
   constexpr int RB = KC * 2;                    // 64 B per row and plane
-  constexpr int APL = CWW * RB, BPL = ER * RB;   // 16 KiB, 8 KiB
-  constexpr int STG = 2 * APL + 2 * BPL;        // 48 KiB
-  constexpr int NSTG = 3;
-  constexpr int DBYTES = ER * DS * 4;
+  constexpr int APL = CWW * RB, BPL = ER2 * RB;  // 16 KiB, 16 KiB
+  constexpr int STG = 2 * APL + 2 * BPL;        // 64 KiB
+  constexpr int NSTG = 2;
+  constexpr int QR = 64;                        // rows per E-step quarter
+  constexpr int DBYTES = QR * DS * 4;
   constexpr int UN = (NSTG * STG > DBYTES) ? NSTG * STG : DBYTES;
+  constexpr int NPC = STG / 1024 / NW;          // pieces per wave and stage (8)
   __shared__ __attribute__((aligned(16))) char sm[UN];
   __shared__ int s_srow[CWW];
   __shared__ __attribute__((aligned(16))) float s_cn[CWW];
   __shared__ unsigned s_iw0[IMW], s_iw1[IMW];
-  __shared__ int s_gidx[ER];
-  __shared__ float s_xn[ER];
+  __shared__ int s_gidx[ER2];
+  __shared__ float s_xn[ER2];
   __shared__ double s_red[IMW][2];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = a.nb * a.nct;
+  const int RE2 = (a.RE + 1) >> 1;
   const int bid = blockIdx.x, xcd = bid & 7, jb = bid >> 3;
-  const int rt = jb % a.RE, g = (jb / a.RE) * 8 + xcd;
+  const int rt = jb % RE2, g = (jb / RE2) * 8 + xcd;
   if (g >= G) return;
   const int b = g / a.nct, ct = g - b * a.nct;
   const RP R = rp(a, b);
@@ -252,35 +262,26 @@ __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
     s_iw0[i] = T->iw0[i];
     s_iw1[i] = T->iw1[i];
   }
-  if (tid < ER) {
-    const int r = rt * ER + tid;
+  if (tid < ER2) {
+    const int r = rt * ER2 + tid;
     const int gi = idx[min(r, m - 1)];
     s_gidx[tid] = gi;
     s_xn[tid] = a.xnorm[gi];
   }
   __syncthreads();
 
-  // LDS-DMA fill: per stage 48 pieces of 1 KiB (A: 2 planes x 16, B: 2 planes x 8), six per
-  // wave; lane i of a piece writes 16 B at piece base + 16 i, i.e. row i/4, physical chunk
-  // i%4, so it fetches logical chunk (i%4) ^ ((row >> 2) & 3) of its row.  The source rows
-  // are fixed for the workgroup: six 64-bit pointers per lane, advanced by 64 B per stage.
-  // Dummy slots and slots past nslots read a valid X row (their distances are +inf or unread).
+  // LDS-DMA fill: per stage 64 pieces of 1 KiB (A: 2 planes x 16, B: 2 planes x 16), eight per
+  // wave; lane i of a piece writes 16 B at piece base + 16 i, i.e. row i/4, physical chunk i%4,
+  // so it fetches logical chunk (i%4) ^ ((row >> 2) & 3) of its row.  The source rows are fixed
+  // for the workgroup: the per-lane pointers are advanced by 64 B per stage.  Dummy slots and
+  // slots past nslots read a valid X row (their distances are +inf or unread).
   const int S = dpad / KC;
-  const char* psrc[6];
-  int pdst[6];
+  const char* psrc[NPC];
+  int pdst[NPC];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
+  for (int k = 0; k < NPC; ++k) {
     const int pc = wave + NW * k;  // piece of the stage
-    int row, plane, base;
-    if (pc < 32) {
-      plane = pc >> 4;
-      row = (pc & 15) * 16 + (lane >> 2);
-      base = plane * APL + (pc & 15) * 1024;
-    } else {
-      plane = (pc - 32) >> 3;
-      row = ((pc - 32) & 7) * 16 + (lane >> 2);
-      base = 2 * APL + plane * BPL + ((pc - 32) & 7) * 1024;
-    }
+    const int plane = (pc >> 4) & 1, row = (pc & 15) * 16 + (lane >> 2);
     const int chunk = (lane & 3) ^ ((row >> 2) & 3);
     const uint16_t* src;
     if (pc < 32) {
@@ -288,134 +289,136 @@ __global__ __launch_bounds__(NT, 1) void wide_estep(WArgs a) {
       if (sr >= 0) src = a.Xhl + (static_cast<size_t>(sr) * 2 + plane) * dpad;
       else if (sr != INT_MIN) src = R.cenhl + (static_cast<size_t>(-sr - 1) * 2 + plane) * dpad;
       else src = a.Xhl + (static_cast<size_t>(s_gidx[0]) * 2 + plane) * dpad;
+      pdst[k] = plane * APL + (pc & 15) * 1024;
     } else {
       src = a.Xhl + (static_cast<size_t>(s_gidx[row]) * 2 + plane) * dpad;
+      pdst[k] = 2 * APL + plane * BPL + (pc & 15) * 1024;
     }
     psrc[k] = reinterpret_cast<const char*>(src) + 16 * chunk;
-    pdst[k] = base;
   }
   auto issue = [&](int st) __attribute__((always_inline)) {
     const char* ring = sm + (st % NSTG) * STG;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) dma_piece16(psrc[k] + static_cast<size_t>(st) * (2 * KC), ring + pdst[k]);
+    for (int k = 0; k < NPC; ++k) dma_piece16(psrc[k] + static_cast<size_t>(st) * (2 * KC), ring + pdst[k]);
   };
 
   const int ws = wave >> 1, wr = wave & 1, lr = lane & 31, hh = lane >> 5;
   // waves w and w+4 share a SIMD: with ws = w >> 1 they hold different slot groups, so a tile
   // with few slots (k-means++ rounds) still keeps every SIMD's matrix pipe busy
   const bool wact = 64 * ws < nslots;  // wave-uniform
-  v16f acc[2][2];
+  v16f acc[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = v16f{};
+    for (int j = 0; j < 4; ++j) acc[i][j] = v16f{};
   auto fo = [](int row, int c) { return row * RB + 16 * (c ^ ((row >> 2) & 3)); };
   auto compute = [&](int st) __attribute__((always_inline)) {
     if (!wact) return;
     const char* base = sm + (st % NSTG) * STG;
-    // both k-steps' fragments first (16 reads): the second k-step's reads are in flight
-    // under the first k-step's twelve MFMAs
-    h8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      h8 ah[2], al[2], bh[4], bl[4];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int o = fo(64 * ws + 32 * i + lr, 2 * ks + hh);
-        ah[ks][i] = *reinterpret_cast<const h8*>(base + o);
-        al[ks][i] = *reinterpret_cast<const h8*>(base + APL + o);
+        ah[i] = *reinterpret_cast<const h8*>(base + o);
+        al[i] = *reinterpret_cast<const h8*>(base + APL + o);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int o = 2 * APL + fo(64 * wr + 32 * j + lr, 2 * ks + hh);
-        bh[ks][j] = *reinterpret_cast<const h8*>(base + o);
-        bl[ks][j] = *reinterpret_cast<const h8*>(base + BPL + o);
+      for (int j = 0; j < 4; ++j) {
+        const int o = 2 * APL + fo(128 * wr + 32 * j + lr, 2 * ks + hh);
+        bh[j] = *reinterpret_cast<const h8*>(base + o);
+        bl[j] = *reinterpret_cast<const h8*>(base + BPL + o);
       }
-    }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = mfma16(ah[ks][i], bl[ks][j], acc[i][j]);
-          acc[i][j] = mfma16(al[ks][i], bh[ks][j], acc[i][j]);
-          acc[i][j] = mfma16(ah[ks][i], bh[ks][j], acc[i][j]);
+        for (int i = 0; i < 2; ++i) {
+          acc[i][j] = mfma16(ah[i], bl[j], acc[i][j]);
+          acc[i][j] = mfma16(al[i], bh[j], acc[i][j]);
+          acc[i][j] = mfma16(ah[i], bh[j], acc[i][j]);
         }
+    }
   };
-  // stage s: wait for its pieces (stage s+1's six may stay in flight), barrier (everyone's
-  // pieces landed, and every wave is done with stage s-1, whose slot the next issue refills),
-  // issue stage s+2, compute stage s
+  // stage s: wait for its pieces (issued one stage earlier), barrier (everyone's pieces landed,
+  // and every wave is done with stage s-1, whose slot the next issue refills), issue stage s+1,
+  // compute stage s
   issue(0);
-  if (S > 1) issue(1);
   for (int st = 0; st < S; ++st) {
-    if (st + 1 < S) dma_wait_n<6>();
-    else dma_wait_n<0>();
+    dma_wait_n<0>();
     __syncthreads();
-    if (st + 2 < S) issue(st + 2);
+    if (st + 1 < S) issue(st + 1);
     compute(st);
   }
   __syncthreads();
 
-  // distance tile D[row][slot] = |c|^2 - 2 x.c (aliases the stages: the loop ended on a barrier)
+  // per 64-row quarter: the distance tile D[row][slot] = |c|^2 - 2 x.c of its rows (aliases the
+  // stages), then the E-step; thread = (row of the quarter, item group of 8)
   float* D = reinterpret_cast<float*>(sm);
-  if (wact) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int slot0 = 64 * ws + 32 * i + 8 * gq + 4 * hh;
-          const int row = 64 * wr + 32 * j + lr;
-          const float4 c4 = *reinterpret_cast<const float4*>(s_cn + slot0);
-          float4 d;
-          d.x = c4.x - a.dscale * acc[i][j][4 * gq];
-          d.y = c4.y - a.dscale * acc[i][j][4 * gq + 1];
-          d.z = c4.z - a.dscale * acc[i][j][4 * gq + 2];
-          d.w = c4.w - a.dscale * acc[i][j][4 * gq + 3];
-          *reinterpret_cast<float4*>(D + row * DS + slot0) = d;
-        }
-  }
-  __syncthreads();
-
-  // E-step: thread = (row, item group of 4); two waves per group cover the 128 rows
   constexpr float INF = __builtin_huge_valf();
-  const int row = tid & (ER - 1), grp = tid >> 7, w2 = (tid >> 6) & 1;
-  const int r = rt * ER + row;
-  const bool ok = r < m;
-  const float xnr = s_xn[row];
-  const float* drow = D + row * DS;
-  for (int it = grp; it < nitems; it += 4) {
-    const unsigned w0 = s_iw0[it];
-    const int kind = iw_kind(w0), p = iw_prob(w0), off = iw_off(w0);
-    double v = 0.0;
-    if (kind >= IK_RUN) {
-      const int K = iw_K(w0);
-      float best = INF;
-      int lab = 0;
-      for (int c = 0; c < K; c += 4) amin4(*reinterpret_cast<const float4*>(drow + off + c), c, best, lab);
-      if (ok) {
-        R.glab[(static_cast<size_t>(p) * 2 + iw_buf(w0)) * a.lsm + r] = static_cast<uint8_t>(lab);
-        v = static_cast<double>(xnr) + static_cast<double>(best);
-        // the row's squared distance to its centre as the E-step has it (dbuf slot 0 is free once
-        // a problem runs Lloyd): relocate() filters its candidates with it
-        R.dbuf[static_cast<size_t>(p) * a.ndb * a.lsm + r] = xnr + best;
-      }
-    } else {
-      const float dist = fmaxf(xnr + drow[off], 0.f);
-      const unsigned w1 = s_iw1[it];
-      if (ok) {
-        float dm = dist;
-        if (kind == IK_SEED) dm = fminf(R.dbuf[(static_cast<size_t>(p) * a.ndb + ((w1 >> 4) & 15)) * a.lsm + r], dist);
-        R.dbuf[(static_cast<size_t>(p) * a.ndb + ((w1 >> 8) & 15)) * a.lsm + r] = dm;
-        v = static_cast<double>(dm);
+  const int qrow = tid & (QR - 1), grp = tid >> 6;
+  for (int q = 0; q < ER2 / QR; ++q) {
+    if (wact && wr == (q >> 1)) {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * (q & 1) + jj;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq) {
+            const int slot0 = 64 * ws + 32 * i + 8 * gq + 4 * hh;
+            const int row = 32 * jj + lr;
+            const float4 c4 = *reinterpret_cast<const float4*>(s_cn + slot0);
+            float4 d;
+            d.x = c4.x - a.dscale * acc[i][j][4 * gq];
+            d.y = c4.y - a.dscale * acc[i][j][4 * gq + 1];
+            d.z = c4.z - a.dscale * acc[i][j][4 * gq + 2];
+            d.w = c4.w - a.dscale * acc[i][j][4 * gq + 3];
+            *reinterpret_cast<float4*>(D + row * DS + slot0) = d;
+          }
       }
     }
-    v = wave_sum(v);
-    if (lane == 0) s_red[it][w2] = v;
+    __syncthreads();
+    const int lrow = QR * q + qrow;  // row of the 256-row tile
+    const int r = rt * ER2 + lrow;
+    const bool ok = r < m;
+    const float xnr = s_xn[lrow];
+    const float* drow = D + qrow * DS;
+    for (int it = grp; it < nitems; it += NW) {
+      const unsigned w0 = s_iw0[it];
+      const int kind = iw_kind(w0), p = iw_prob(w0), off = iw_off(w0);
+      double v = 0.0;
+      if (kind >= IK_RUN) {
+        const int K = iw_K(w0);
+        float best = INF;
+        int lab = 0;
+        for (int c = 0; c < K; c += 4) amin4(*reinterpret_cast<const float4*>(drow + off + c), c, best, lab);
+        if (ok) {
+          R.glab[(static_cast<size_t>(p) * 2 + iw_buf(w0)) * a.lsm + r] = static_cast<uint8_t>(lab);
+          v = static_cast<double>(xnr) + static_cast<double>(best);
+          // the row's squared distance to its centre as the E-step has it (dbuf slot 0 is free
+          // once a problem runs Lloyd): relocate() filters its candidates with it
+          R.dbuf[static_cast<size_t>(p) * a.ndb * a.lsm + r] = xnr + best;
+        }
+      } else {
+        const float dist = fmaxf(xnr + drow[off], 0.f);
+        const unsigned w1 = s_iw1[it];
+        if (ok) {
+          float dm = dist;
+          if (kind == IK_SEED) dm = fminf(R.dbuf[(static_cast<size_t>(p) * a.ndb + ((w1 >> 4) & 15)) * a.lsm + r], dist);
+          R.dbuf[(static_cast<size_t>(p) * a.ndb + ((w1 >> 8) & 15)) * a.lsm + r] = dm;
+          v = static_cast<double>(dm);
+        }
+      }
+      v = wave_sum(v);  // the 64 rows of the quarter, in the 128-row form's lane order
+      if (lane == 0) s_red[it][q & 1] = v;
+    }
+    __syncthreads();
+    // a 128-row half done: its per-item partial, as the 128-row form wrote it
+    const int rth = 2 * rt + (q >> 1);
+    if ((q & 1) && tid < nitems && rth < a.RE)
+      R.part[(static_cast<size_t>(ct) * IMW + tid) * a.RE + rth] = s_red[tid][0] + s_red[tid][1];
   }
-  __syncthreads();
-  if (tid < nitems) R.part[(static_cast<size_t>(ct) * IMW + tid) * a.RE + rt] = s_red[tid][0] + s_red[tid][1];
 }
 
 // ============================================================================================
@@ -1561,7 +1564,7 @@ extern "C" int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* 
     hipLaunchKernelGGL(wide_init, dim3(nb), dim3(NT), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail("init launch", e);
     const int G = nb * L.nct;
-    const unsigned eblocks = static_cast<unsigned>(8 * L.RE * ((G + 7) / 8));
+    const unsigned eblocks = static_cast<unsigned>(8 * ((L.RE + 1) / 2) * ((G + 7) / 8));  // 256-row E tiles
     const unsigned mblocks = static_cast<unsigned>(G * L.DT);
     for (long long round = 0;; ++round) {
       int act = 0;

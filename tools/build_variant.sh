@@ -13,6 +13,7 @@ cp "$SRC" $W/consensus_clustering_amd/csrc/kmeans.hip
 [ -n "$CO_SRC" ] && cp "$CO_SRC" $W/consensus_clustering_amd/csrc/coassoc.hip  # a coassoc.hip variant (with REBUILD=coassoc)
 [ -n "$PR_SRC" ] && cp "$PR_SRC" $W/consensus_clustering_amd/csrc/predict.hip  # a predict.hip variant (with REBUILD=predict)
 [ -n "$F64_SRC" ] && cp "$F64_SRC" $W/consensus_clustering_amd/csrc/kmeans_f64.hip  # a kmeans_f64.hip variant (with REBUILD=kmeans_f64)
+[ -n "$WIDE_SRC" ] && cp "$WIDE_SRC" $W/consensus_clustering_amd/csrc/kmeans_wide.hip  # a kmeans_wide.hip variant (with REBUILD=kmeans_wide)
 mkdir -p $W/build
 cp $REPO/build/ccmi/*.o $W/build/ 2>/dev/null || true  # unchanged objects are reused (kmeans.o rebuilds)
 for o in kmeans $REBUILD; do rm -f $W/build/$o.o; done  # REBUILD="coassoc ...": objects whose flags change
