@@ -378,6 +378,7 @@ def main():
     km_ms_tot, km_launches = float(ktime[0]), max(float(ktime[1]), 1.0)
     achieved = flops / (km_ms_tot * 1e-3) / 1e12 if km_ms_tot > 0 else 0.0
     achieved_m = (flops + mstep_flops) / (km_ms_tot * 1e-3) / 1e12 if km_ms_tot > 0 else 0.0
+    exec_flops = 2.0 * d * 32 * 32 * float(st[5]) if km_kernel == "cc_kmeans_batched" else 0.0
     clusterings = cfg["H"] * len(cfg["Ks"]) * args.steps
     value = clusterings / elapsed
     # co-association: OPS_M = sum_K 2 P H K per fit (channel padding and the
@@ -436,6 +437,11 @@ def main():
                 "peak_note": "f16 dense MFMA peak 2516.6 TF / 3 (f32-class product = 3 f16 MFMAs)",
                 "flops_note": "FLOP_KM of SURVEY.md §8d: 2*d per Lloyd and k-means++ distance product",
                 "sweeps": float(st[4]), "slot_tile_row_tiles": float(st[5]),
+                # executed distance products: every 32-row x 32-slot tile a sweep computes, padding
+                # slots (K rounded up to 4 per problem, tiles to 32 slots) included; batched engine only
+                "executed_flops_per_launch": (exec_flops / km_launches) if exec_flops else None,
+                "frac_executed": (checked_frac(exec_flops / (km_ms_tot * 1e-3) / 1e12, KMEANS_PEAK_TF,
+                                               "k-means executed") if exec_flops and km_ms_tot > 0 else None),
                 "relocations": float(st[3]),
                 "traffic": traffic,
                 "flops_per_launch": flops / km_launches,
