@@ -342,15 +342,22 @@ def main():
     engine.TIMERS = {}
     stats = torch.zeros(128, dtype=torch.int64, device=dev)
     t0 = time.perf_counter()
+    # each fit's counters are summed after the timed region: a torch add here would put the lazy
+    # load of its kernel (~70 ms, once per process) inside the second step
+    step_ends, fit_totals, step_stats = [], [], []
     for i in range(args.steps):
-        cc.fit(Xd)
-        stats += cc.kmeans_stats_
+        cc.fit(Xd)  # synchronous: returns after its host post-processing
+        step_ends.append(time.perf_counter())
+        fit_totals.append(cc.timings_["total"])
+        step_stats.append(cc.kmeans_stats_)
         if rank == 0:
             print(f"[bench] step {i} queued", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    for st_i in step_stats:
+        stats += st_i
     timers = engine.timer_summary(engine.TIMERS)
     engine.TIMERS = None
 
@@ -468,6 +475,8 @@ def main():
             "kernels_ms_per_step": {k: v[1] / args.steps for k, v in timers.items()},
             "kernel_launches_per_step": {k: v[0] / args.steps for k, v in timers.items()},
             "fit_timings_s": {k: round(v, 4) for k, v in cc.timings_.items()},
+            "step_ms": [round(1e3 * (b - a), 1) for a, b in zip([t0] + step_ends[:-1], step_ends)],
+            "fit_total_ms": [round(1e3 * v, 1) for v in fit_totals],
             "partial": bool(cc.partial_),
         }
         if world == 1 and not args.no_consensus_roofline and not args.rehearse:

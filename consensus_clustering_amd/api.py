@@ -172,6 +172,10 @@ class ConsensusClustering:
         if H > 0 and (int(self.random_state) < 0 or int(self.random_state) + H - 1 > 2**32 - 1):
             raise ValueError("Seed must be between 0 and 2**32 - 1")
         rank, W = dist.world()
+        # a refit replaces the previous results: their device buffers are dropped first, so the
+        # new label matrix and indices reuse that memory instead of growing the pool by a set
+        self.labels_ = self._idx_dev = self._idx_host = None
+        self.kmeans_inertia_ = self.kmeans_n_iter_ = self.kmeans_stats_ = None
         self.partial_ = False
         if self._rehearsal is not None:
             # one-GPU rehearsal of rank r's share of a W-rank fit (bench tooling only): the
