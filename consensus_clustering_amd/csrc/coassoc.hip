@@ -1032,7 +1032,7 @@ __global__ void copy_label_columns_kernel(const uint8_t* __restrict__ src, int64
 }
 
 // C = f32(M) / f32(f64(I) + 1e-6), C_ii = 1 (CC.py:372-373), one HBM stream of 12 bytes per
-// element.  n % 4 == 0 (every row 16-B aligned): a workgroup per row (grid-stride over rows), each
+// element.  n % 4 == 0 and 16-B aligned M, I, C (then every row is): a workgroup per row (grid-stride over rows), each
 // thread 4 elements per access (dwordx4 loads of M and I, one dwordx4 store), 4 accesses in flight;
 // no per-element index division.  Otherwise the flat form below.
 typedef int cc_i4 __attribute__((ext_vector_type(4)));
@@ -1292,7 +1292,9 @@ extern "C" int cc_consensus(const int32_t* M, const int32_t* I, int n, float* C,
     return CC_ERR_ARG;
   }
   const int64_t total = static_cast<int64_t>(n) * n;
-  if (n % 4 == 0) {
+  const bool al16 = ((reinterpret_cast<uintptr_t>(M) | reinterpret_cast<uintptr_t>(I) |
+                     reinterpret_cast<uintptr_t>(C)) & 15) == 0;  // the row form's 16-B accesses
+  if (n % 4 == 0 && al16) {
     const int blocks = std::min(n, 8192);  // 32 resident 256-thread workgroups per CU
     hipLaunchKernelGGL(consensus_rows_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), M, I, n, C);
   } else {

@@ -160,6 +160,23 @@ def test_consensus_matrix_kernel(n):
     np.testing.assert_array_equal(C, O.consensus_matrix(M.astype(np.uint16), I.astype(np.uint16)))
 
 
+def test_consensus_matrix_kernel_unaligned():
+    # n % 4 == 0 but M 4-B aligned only (a view one element into its buffer): cc_consensus
+    # must take the flat form, whose accesses are 4-B
+    dev = engine.require_gpu()
+    n = 2052
+    rng = np.random.default_rng(1)
+    I = rng.integers(0, 1001, size=(n, n)).astype(np.int32)
+    I = np.maximum(I, I.T)
+    M = (I * rng.random((n, n))).astype(np.int32)
+    buf = torch.empty(n * n + 1, dtype=torch.int32, device=dev)
+    Mv = buf[1:].view(n, n)
+    Mv.copy_(torch.from_numpy(M))
+    assert Mv.data_ptr() % 16 != 0
+    C = engine.consensus(Mv, torch.from_numpy(I).to(dev)).cpu().numpy()
+    np.testing.assert_array_equal(C, O.consensus_matrix(M.astype(np.uint16), I.astype(np.uint16)))
+
+
 @pytest.mark.parametrize("H,K", [(37, 3), (256, 10), (300, 7), (1000, 20), (1500, 5)])
 def test_threshold_table_binning_is_exact(H, K):
     """cc_coassoc's division-free binning (cc_bin_table thresholds) gives the same 20 counts as
