@@ -1092,6 +1092,10 @@ int check_common(const char* fn, const void* labels, int n, int ldl, int Hpad, i
     cc::set_error(std::string(fn) + ": bad labels/n/ldl/Hpad (Hpad % 128 == 0, ldl >= Hpad, ldl % 16 == 0)");
     return CC_ERR_ARG;
   }
+  if (reinterpret_cast<uintptr_t>(labels) & 15) {
+    cc::set_error(std::string(fn) + ": labels_nh must be 16-B aligned (16-B row loads)");
+    return CC_ERR_ARG;
+  }
   if (Hpad > 65535) {
     cc::set_error(std::string(fn) + ": Hpad > 65535 overflows the uint16 co-sampling tiles");
     return CC_ERR_ARG;
@@ -1165,8 +1169,8 @@ extern "C" int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, in
   int rc = check_common("cc_cosample", labels_nh, n, ldl, Hpad, tile_begin, tile_end);
   if (rc) return rc;
   if (tile_end == tile_begin) return CC_OK;  // an empty band (a rank with no tiles)
-  if (!I_tiles) {
-    cc::set_error("cc_cosample: I_tiles is NULL");
+  if (!I_tiles || (reinterpret_cast<uintptr_t>(I_tiles) & 15)) {
+    cc::set_error("cc_cosample: I_tiles is NULL or not 16-B aligned");
     return CC_ERR_ARG;
   }
   const int64_t ntl = tile_end - tile_begin;
@@ -1234,6 +1238,10 @@ extern "C" int cc_coassoc(const int8_t* labels_nh, int n, int ldl, int Hpad, int
   if (tile_end == tile_begin) return CC_OK;  // an empty band (a rank with no tiles)
   if (!I_tiles || !edges || !bin_counts) {
     cc::set_error("cc_coassoc: I_tiles, edges and bin_counts are required");
+    return CC_ERR_ARG;
+  }
+  if ((reinterpret_cast<uintptr_t>(I_tiles) | reinterpret_cast<uintptr_t>(bin_table)) & 15) {
+    cc::set_error("cc_coassoc: I_tiles and bin_table must be 16-B aligned (16-B tile and table copies)");
     return CC_ERR_ARG;
   }
   if (bin_table && (table_rows < Hpad + 1 || table_rows > BT_MAX_ROWS)) {

@@ -106,7 +106,8 @@ int cc_copy_label_columns(const uint8_t* src, int64_t ld_src, int col_src, uint8
 
 /* Co-sampling counts I_ij = #{h : i and j both sampled} for the tiles
  * [tile_begin, tile_end) of the upper-triangle tiling (CC.py:264).
- * labels_nh: [n][ldl] int8, 0xFF = not sampled; Hpad (multiple of 128, <= ldl) columns used.
+ * labels_nh: [n][ldl] int8, 0xFF = not sampled; Hpad (multiple of 128, <= ldl) columns used;
+ *            16-B aligned, like I_tiles and bin_table below (device allocations are).
  * I_tiles:   [tile_end - tile_begin][CC_TILE*CC_TILE] uint16, accumulator order (device-private).
  * I_full:    optional [n][n] int32 (both triangles), may be NULL. */
 int cc_cosample(const int8_t* labels_nh, int n, int ldl, int Hpad, int64_t tile_begin,
