@@ -2204,6 +2204,10 @@ extern "C" int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const floa
     cc::set_error("cc_kmeans_batched: bad arguments");
     return CC_ERR_ARG;
   }
+  if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Xhl) | reinterpret_cast<uintptr_t>(workspace)) & 15) != 0) {
+    cc::set_error("cc_kmeans_batched: X, Xhl and the workspace must be 16-B aligned (16-B row and LDS-DMA loads)");
+    return CC_ERR_ARG;
+  }
   if (dpad != 32 && dpad != 64 && dpad != 128) {
     cc::set_error("cc_kmeans_batched: dpad must be 32, 64 or 128 (d <= 128 in this build)");
     return CC_ERR_UNSUPPORTED;

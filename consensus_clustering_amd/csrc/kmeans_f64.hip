@@ -1456,6 +1456,10 @@ extern "C" int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_h
     cc::set_error("cc_kmeans_f64: bad arguments");
     return CC_ERR_ARG;
   }
+  if ((reinterpret_cast<uintptr_t>(X) & 7) != 0 || (reinterpret_cast<uintptr_t>(workspace) & 15) != 0) {
+    cc::set_error("cc_kmeans_f64: X must be 8-B and the workspace 16-B aligned");
+    return CC_ERR_ARG;
+  }
   int kmax = 1, tmax = 0;
   for (int i = 0; i < nK; ++i) {
     if (Ks[i] < 1 || Ks[i] > KMAX || Ks[i] > m) {

@@ -1471,6 +1471,10 @@ extern "C" int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* 
     cc::set_error("cc_kmeans_wide: bad arguments");
     return CC_ERR_ARG;
   }
+  if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Xhl) | reinterpret_cast<uintptr_t>(workspace)) & 15) != 0) {
+    cc::set_error("cc_kmeans_wide: X, Xhl and the workspace must be 16-B aligned (16-B row and LDS-DMA loads)");
+    return CC_ERR_ARG;
+  }
   WL L;
   if (!wide_layout(m, dpad, Ks, nK, n_init, L)) return CC_ERR_UNSUPPORTED;
   int kmax = 0, tmax = 0;

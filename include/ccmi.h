@@ -237,7 +237,8 @@ int cc_split_f16(const float* X, int n, int dpad, int scale_exp, uint16_t* Xhl, 
  *            32-slot column tiles x row tiles swept}
  *  grid      workgroups (<= units; one per CU is the intended size)
  *  seedmax   problems of a unit seeding concurrently (1..32)
- *  All pointers except units_host are device pointers. */
+ *  All pointers except units_host are device pointers; X, Xhl and workspace 16-B aligned
+ *  (device allocations are; CC_ERR_ARG otherwise). */
 int cc_kmeans_batched(const float* X, const uint16_t* Xhl, const float* xnorm, int n, int dreal,
                       int dpad, int scale_exp, const int32_t* idx_hm, int H, int m, int h_begin,
                       int h_end, const int32_t* units, const int32_t* units_host, int nU,
@@ -273,7 +274,7 @@ int cc_kmeans_wide(const float* X, const uint16_t* Xhl, const float* xnorm, int 
  * (resample, K) unit (or pair of K's); inertia is float64 here.  Workspace from
  * cc_kmeans_f64_workspace_bytes(m, d, Ks, nK, grid, nh): grid workgroup areas and min(grid, nh)
  * per-resample slots for nh = h_end - h_begin (resamples beyond grid run in further launches on
- * the same stream). */
+ * the same stream).  X 8-B and workspace 16-B aligned. */
 size_t cc_kmeans_f64_workspace_bytes(int m, int d, const int32_t* Ks, int nK, int grid, int nh);
 
 int cc_kmeans_f64(const double* X, int n, int d, const int32_t* idx_hm, int H, int m, int h_begin,
