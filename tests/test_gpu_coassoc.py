@@ -278,3 +278,32 @@ def test_coassoc_all_streams_is_exact(streams):
     np.testing.assert_array_equal(counts.cpu().numpy(), counts_ref)
     for j in range(len(Ks)):
         np.testing.assert_array_equal(Ms[j].cpu().numpy(), M_ref[j])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fit_path_counts_random_shapes(seed):
+    """The fit's own calls (co-sampling tiles without the n x n matrices, then coassoc_all over the
+    side streams: interior tiles take the staged-table binning) on seeded random shapes -- n off
+    the tile grid, H across the three table forms, K from 2 to 40 -- against the oracle's
+    histogram of C."""
+    dev = engine.require_gpu()
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(257, 1200))
+    H = [1, 129, 256, 300, 700, 1100][seed]  # table forms: triangle (H <= ~420), pairs, uint16
+    frac = float(rng.uniform(0.5, 1.0))
+    Ks = sorted({int(k) for k in rng.integers(2, 41, size=3)})
+    Ks = [K for K in Ks if H * K <= 9000] or [2, int(rng.integers(3, 9))]
+    idx, labs = _random_case(n, H, frac, Ks, seed=seed)
+    L, Hpad = _device_labels(idx, labs, n, H, dev)
+    nt = engine.num_tiles(n)
+    I_tiles, _ = engine.cosample(L[0], n, Hpad, 0, nt, want_full=False)
+    counts = torch.zeros((len(Ks), 20), dtype=torch.int64, device=dev)
+    engine.coassoc_all(L, n, Hpad, Ks, 0, nt, I_tiles, counts, None, streams=3)
+    counts = counts.cpu().numpy()
+    I_ref = O.cosample_matrix(idx.astype(np.int64), n)
+    iu = np.triu_indices(n, 1)
+    for j, K in enumerate(Ks):
+        M_ref = O.coassoc_matrix(idx.astype(np.int64), labs[j].astype(np.int64), K, n)
+        C = O.consensus_matrix(M_ref.astype(np.uint16), I_ref.astype(np.uint16))
+        pair, _ = np.histogram(C[iu], bins=20, range=(0, 1))
+        np.testing.assert_array_equal(counts[j], pair, err_msg=f"n={n} H={H} K={K}")
