@@ -30,8 +30,10 @@ Three kinds of fixture under tests/golden/sk/:
   through the reference's co-association and histogram (CC.py:284-290, :338-344, numpy on row
   blocks, the same per-element C = float32(M) / float32(I + 1e-6) and numpy.histogram binning,
   counts summed over blocks) -> the 20 strict-upper pair counts per K, plus every label
-  vector's digest.  The float64 fits' counts give the reference's own float32 / float64 PAC
-  spread, against which the engine's |dPAC| is bounded.
+  vector's digest.  The float64 fits' counts, and those of PAC_NUDGES float32 runs on
+  2^-22-nudged inputs (``pair_counts_nudge``), give the reference's own PAC spread under
+  rounding, against which the engine's |dPAC| is bounded.  PAC_NUDGES_ONLY=1 adds the nudged
+  runs to existing PAC fixtures.
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_sk_fixtures.py [case ...]
 """
@@ -336,6 +338,47 @@ def make_f64(ex, case="f64_c3shape"):
     print(f"{case}: {len(res)} fits ({time.time() - t0:.0f} s); n_iter {nit.min()}..{nit.max()}", flush=True)
 
 
+PAC_NUDGES = 2  # extra reference runs per PAC case: the float32 fit on 2^-22-nudged inputs
+
+
+def _nudge_task(args):
+    """sklearn's float32 fit of one (K, h) on rows nudged by a random-sign 2^-22 relative step
+    (draw v), the rounding perturbation sk_parity's per-problem cloud uses."""
+    case, K, h, v = args
+    X = _X[case]
+    spec = PAC_CASES[case]
+    rows = X[indices(X.shape[0], spec["seed"], h)]
+    sign = np.random.default_rng([v, K, h]).choice(np.array([-1.0, 1.0]), size=rows.shape)
+    lab = _fit((rows.astype(np.float64) * (1.0 + sign * 2.0 ** -22)).astype(np.float32), K, spec["seed"])[0]
+    return K, h, lab
+
+
+def add_pac_nudges(case, ex):
+    """Add pair_counts_nudge [PAC_NUDGES, nK, 20] to an existing PAC fixture: the reference's
+    PAC under input rounding, next to its float64 run, for the engine's |dPAC| bound."""
+    path = os.path.join(OUT, f"{case}.npz")
+    with np.load(path, allow_pickle=False) as z:
+        old = {k: z[k] for k in z.files}
+    spec = PAC_CASES[case]
+    Ks, H = spec["Ks"], spec["H"]
+    n, m = _X[case].shape[0], int(0.8 * _X[case].shape[0])
+    t0 = time.time()
+    out = np.zeros((PAC_NUDGES, len(Ks), 20), dtype=np.int64)
+    for v in range(PAC_NUDGES):
+        labs = {K: np.zeros((H, m), dtype=np.int8) for K in Ks}
+        for K, h, lab in ex.map(_nudge_task, [(case, K, h, v) for K in Ks for h in range(H)]):
+            labs[K][h] = lab
+        for K, c in ex.map(_pair_counts_task, [(case, K, labs[K]) for K in Ks]):
+            out[v, Ks.index(K)] = c
+        assert np.all(out[v].sum(axis=1) == n * (n - 1) // 2)
+        print(f"  {case}: nudge draw {v} ({time.time() - t0:.0f} s)", flush=True)
+    meta = json.loads(str(old["meta"]))
+    meta["nudge_draws"] = PAC_NUDGES
+    old["meta"] = np.array(json.dumps(meta))
+    old["pair_counts_nudge"] = out
+    np.savez_compressed(path, **old)
+
+
 def make_pac(case, ex):
     spec = PAC_CASES[case]
     X = _X[case]
@@ -379,7 +422,11 @@ def main(argv):
             if c in CASES:
                 make_classify(c, ex)
             elif c in PAC_CASES:
-                make_pac(c, ex)
+                if os.environ.get("PAC_NUDGES_ONLY"):
+                    add_pac_nudges(c, ex)
+                else:
+                    make_pac(c, ex)
+                    add_pac_nudges(c, ex)
             else:
                 make_f64(ex, c)
 

@@ -34,11 +34,16 @@ pytestmark = pytest.mark.gpu
 # (observed, round 4: |dPAC| <= 3.9e-4 at n = 3000 and 1.4e-3 at the C2 shape; max |dC| 0.077)
 F32_MAX_DPAC = 2e-3
 F32_MAX_DC = 0.1
-# C2 / C3 shapes: |dPAC| per K within max(F32_MAX_DPAC, F32_SPREAD_FACTOR x the reference's own
-# float32 / float64 spread at that K).  At the C2 shape, K = 8, sklearn's float64 labels put PAC
-# 2.48e-3 away from its float32 labels (tests/golden/sk/pac_c2_h50.npz); the engine's float32-class
-# arithmetic is held to the same precision class, not to one rounding.
+# C2 / C3 shapes: |dPAC| per K within max(PAC_SPREAD_FLOOR, F32_SPREAD_FACTOR x the reference's
+# own PAC spread under rounding at that K): the largest |dPAC| of sklearn's float64 run and of its
+# float32 runs on 2^-22-nudged inputs (two draws) against its float32 run.  At the C2 shape, K = 8,
+# the float64 labels move PAC by 2.48e-3 and a nudge by 3.05e-3; at the C3 shape sklearn's own
+# nudges move PAC by up to 7.9e-3 at K = 4 (tests/golden/sk/pac_*.npz).  The engine's float32-class
+# arithmetic is held to the same precision class, not to one rounding.  The floor (1e-4, the
+# round-6 bound; 2e-3 before the nudged runs existed) covers K whose three reference runs happen
+# to agree closely (C2 K = 11: 4.1e-5 against 1.1e-5).
 F32_SPREAD_FACTOR = 1.5
+PAC_SPREAD_FLOOR = 1e-4
 
 
 def _fit(pf, **kw):
@@ -174,18 +179,19 @@ def _pac_against_fixture(case):
         same = sum(digest(col[idx[h], h].astype(np.int8)) == f["digest32"][j, h] for h in range(H))
         same_total += same
         pac_ref[K] = float(_pac_of_counts(f["pair_counts"][j], n))
-        # the reference's own precision spread at this K: sklearn float64 labels' PAC against
-        # its float32 labels' PAC
-        spread = abs(float(_pac_of_counts(f["pair_counts64"][j], n)) - pac_ref[K])
+        # the reference's own precision spread at this K: sklearn's float64 labels' PAC and its
+        # nudged-input float32 runs' PACs against its float32 labels' PAC
+        spread = max(abs(float(_pac_of_counts(c, n)) - pac_ref[K])
+                     for c in [f["pair_counts64"][j]] + [v[j] for v in f["pair_counts_nudge"]])
         dpac = abs(float(cc.pac_area_[K]) - pac_ref[K])
         report.append((K, same, round(dpac, 6), round(spread, 6)))
         if K <= kt:
             assert same == H, (K, same)
             np.testing.assert_array_equal(cc.pair_counts_[K], f["pair_counts"][j], err_msg=f"K={K}")
-        if dpac > max(F32_MAX_DPAC, F32_SPREAD_FACTOR * spread):
+        if dpac > max(PAC_SPREAD_FLOOR, F32_SPREAD_FACTOR * spread):
             over.append((K, dpac, spread))
     print(f"{case}: {same_total}/{len(Ks) * H} label vectors identical to sklearn's float32 fit; "
-          f"(K, identical of {H}, |dPAC|, sklearn f64-vs-f32 |dPAC|):", report, "best K", cc.best_k_,
+          f"(K, identical of {H}, |dPAC|, sklearn's own |dPAC| under rounding):", report, "best K", cc.best_k_,
           post.best_k(pac_ref))
     assert not over, over
     assert cc.best_k_ == post.best_k(pac_ref)
