@@ -32,8 +32,8 @@ Three kinds of fixture under tests/golden/sk/:
   counts summed over blocks) -> the 20 strict-upper pair counts per K, plus every label
   vector's digest.  The float64 fits' counts, and those of PAC_NUDGES float32 runs on
   2^-22-nudged inputs (``pair_counts_nudge``), give the reference's own PAC spread under
-  rounding, against which the engine's |dPAC| is bounded.  PAC_NUDGES_ONLY=1 adds the nudged
-  runs to existing PAC fixtures.
+  rounding, against which the engine's |dPAC| is bounded (``digest_nudge``: their label
+  digests).  PAC_NUDGES_ONLY=1 adds the nudged runs to existing PAC fixtures.
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_sk_fixtures.py [case ...]
 """
@@ -364,10 +364,12 @@ def add_pac_nudges(case, ex):
     n, m = _X[case].shape[0], int(0.8 * _X[case].shape[0])
     t0 = time.time()
     out = np.zeros((PAC_NUDGES, len(Ks), 20), dtype=np.int64)
+    dig = np.full((PAC_NUDGES, len(Ks), H), "", dtype="U64")
     for v in range(PAC_NUDGES):
         labs = {K: np.zeros((H, m), dtype=np.int8) for K in Ks}
         for K, h, lab in ex.map(_nudge_task, [(case, K, h, v) for K in Ks for h in range(H)]):
             labs[K][h] = lab
+            dig[v, Ks.index(K), h] = digest(lab)
         for K, c in ex.map(_pair_counts_task, [(case, K, labs[K]) for K in Ks]):
             out[v, Ks.index(K)] = c
         assert np.all(out[v].sum(axis=1) == n * (n - 1) // 2)
@@ -376,6 +378,7 @@ def add_pac_nudges(case, ex):
     meta["nudge_draws"] = PAC_NUDGES
     old["meta"] = np.array(json.dumps(meta))
     old["pair_counts_nudge"] = out
+    old["digest_nudge"] = dig
     np.savez_compressed(path, **old)
 
 

@@ -190,6 +190,10 @@ def _pac_against_fixture(case):
             np.testing.assert_array_equal(cc.pair_counts_[K], f["pair_counts"][j], err_msg=f"K={K}")
         if dpac > max(PAC_SPREAD_FLOOR, F32_SPREAD_FACTOR * spread):
             over.append((K, dpac, spread))
+    if "digest_nudge" in f:  # sklearn against itself: its nudged-input runs' labels equal to its own
+        self_same = [int((f["digest_nudge"][:, j, :] == f["digest32"][j][None, :]).sum()) for j in range(len(Ks))]
+        print(f"{case}: sklearn's nudged-input float32 runs identical to its own float32 labels, per K "
+              f"(of {f['digest_nudge'].shape[0] * H}):", dict(zip(Ks, self_same)))
     print(f"{case}: {same_total}/{len(Ks) * H} label vectors identical to sklearn's float32 fit; "
           f"(K, identical of {H}, |dPAC|, sklearn's own |dPAC| under rounding):", report, "best K", cc.best_k_,
           post.best_k(pac_ref))
