@@ -16,6 +16,9 @@ bin_edges / pac_area, and SHA-256 digests of the reference's iij, of every K's m
 K's cij.  The GPU test rebuilds M from the captured labels with the bit-exact co-association
 and checks it against the digests first, so the reference's C is available exactly.
 
+The float32 fixture also holds the reference's own runs on 2^-22-nudged inputs
+(``pac_area_nudge``, ``max_dc_nudge``; NUDGES_ONLY=1 adds them to an existing fixture).
+
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_parity_blobs.py
 """
 from __future__ import annotations
@@ -89,10 +92,62 @@ def save(name, X):
     print(name, "best_k", meta["best_k"], "pac:", dict(zip(Ks, np.round(pac, 6))))
 
 
+NUDGES = 2  # reference runs on float32 inputs nudged by a random-sign 2^-22 relative step
+
+
+def add_nudges(name="parity_blobs_n3000_f32"):
+    """The reference itself on 2^-22-nudged copies of the float32 input (NUDGES draws): its PAC
+    per K and its max |dC| against the un-nudged run's C, the reference's own spread under one
+    input rounding, which bounds the float32-class engine (tests/test_gpu_parity_blobs.py).  The
+    un-nudged C is rebuilt from the fixture's captured labels with the oracle and checked
+    against the stored digests first."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import cc_oracle as O
+
+    path = os.path.join(HERE, f"{name}.npz")
+    with np.load(path, allow_pickle=False) as z:
+        arrays = {k: z[k] for k in z.files}
+    meta = json.loads(str(arrays["meta"]))
+    X, idx, labels = arrays["X"], arrays["indices"].astype(np.int64), arrays["labels"]
+    Ks = [int(k) for k in arrays["K_range"]]
+    n = X.shape[0]
+    dt = O.reference_dtype(H)
+    I = O.cosample_matrix(idx, n).astype(dt)
+    assert digest(I) == meta["iij_sha256"]
+    C_ref = {}
+    for j, K in enumerate(Ks):
+        M = O.coassoc_matrix(idx, labels[j].astype(np.int64), K, n).astype(dt)
+        assert digest(M) == meta["mij_sha256"][str(K)], K
+        C_ref[K] = O.consensus_matrix(M, I)
+        assert digest(C_ref[K]) == meta["cij_sha256"][str(K)], K
+    pac = np.zeros((NUDGES, len(Ks)))
+    max_dc = np.zeros((NUDGES, len(Ks)))
+    for v in range(NUDGES):
+        sign = np.random.default_rng([v, 3000]).choice(np.array([-1.0, 1.0]), size=X.shape)
+        Xv = (X.astype(np.float64) * (1.0 + sign * 2.0 ** -22)).astype(np.float32)
+        cc, idx_v, _ = run_reference(Xv, K_RANGE, H, FRAC, SEED, kmeans_factory)
+        assert np.array_equal(idx_v, idx)
+        for j, K in enumerate(Ks):
+            d = cc.cdf_at_K_data[K]
+            pac[v, j] = d["pac_area"]
+            max_dc[v, j] = float(np.abs(d["cij"].astype(np.float64) - C_ref[K]).max())
+        print(f"{name} nudge {v}: |dPAC|", dict(zip(Ks, np.round(np.abs(pac[v] - arrays["pac_area"]), 6))),
+              "max|dC|", dict(zip(Ks, np.round(max_dc[v], 4))), flush=True)
+    arrays["pac_area_nudge"] = pac
+    arrays["max_dc_nudge"] = max_dc
+    meta["nudge_draws"] = NUDGES
+    arrays["meta"] = np.array(json.dumps(meta))
+    np.savez_compressed(path, **arrays)
+
+
 def main():
+    if os.environ.get("NUDGES_ONLY"):
+        add_nudges()
+        return
     X = blobs()
     save("parity_blobs_n3000_f64", X)
     save("parity_blobs_n3000_f32", X.astype(np.float32))
+    add_nudges()
 
 
 if __name__ == "__main__":

@@ -11,7 +11,8 @@ exactly.
   every K's mij and cij, hist, cdf and PAC identical to the reference, the same best K.
 * float32 input (the f16 hi/lo MFMA engine: sklearn float32's accuracy class, not its rounding):
   identical M, C, hist, cdf and PAC for K <= k_true, the same best K, and for K > k_true |dPAC|
-  and max |dC| reported and bounded.  sklearn's float32 fit is not reproducible there even by
+  and max |dC| bounded by the reference's own movement under 2^-22 input nudges (two reference
+  runs stored in the fixture).  sklearn's float32 fit is not reproducible there even by
   sklearn (tests/test_parity_fixtures.py, tools/sklearn_self_parity.py).
 * the C2 shape (n = 10 000, d = 64, k_true = 6, K = 2..15) at H = 50 and the C3 shape
   (n = 50 000, d = 128, k_true = 8, K = 2..20) at H = 16: sklearn's float32 labels of every
@@ -19,8 +20,8 @@ exactly.
   container (tests/golden/make_sk_fixtures.py, committed as tests/golden/sk/pac_*.npz: pair counts
   per K and every label vector's digest), give the reference's PAC per K; the engine's own fit
   must have identical labels and pair counts for K <= k_true, |dPAC| above within
-  max(F32_MAX_DPAC, F32_SPREAD_FACTOR x sklearn's own float32 / float64 |dPAC| at that K), and the
-  same best K.
+  max(PAC_SPREAD_FLOOR, F32_SPREAD_FACTOR x sklearn's own |dPAC| under rounding at that K: its
+  float64 run and two nudged-input float32 runs), and the same best K.
 """
 import numpy as np
 import pytest
@@ -30,10 +31,12 @@ from tests.conftest import digest, load_fixture
 
 pytestmark = pytest.mark.gpu
 
-# float32 input, K > k_true: bounds on the engine's distance from the reference's result
-# (observed, round 4: |dPAC| <= 3.9e-4 at n = 3000 and 1.4e-3 at the C2 shape; max |dC| 0.077)
-F32_MAX_DPAC = 2e-3
-F32_MAX_DC = 0.1
+# float32 input, K > k_true, n = 3000: the engine's distance from the reference's result is
+# bounded by the reference's own distance from itself under one input rounding.  The fixture holds
+# two reference runs on 2^-22-nudged inputs (make_parity_blobs.py add_nudges).  Their largest
+# |dPAC| over K (3.9e-4, K = 8) times F32_SPREAD_FACTOR bounds the engine's |dPAC| at every K, and
+# their largest max |dC| (0.097) bounds the engine's max |dC|.  Observed, round 6: 3.9e-4 and
+# 0.077.  These replace the constants 2e-3 and 0.1 of rounds 4-5.
 # C2 / C3 shapes: |dPAC| per K within max(PAC_SPREAD_FLOOR, F32_SPREAD_FACTOR x the reference's
 # own PAC spread under rounding at that K): the largest |dPAC| of sklearn's float64 run and of its
 # float32 runs on 2^-22-nudged inputs (two draws) against its float32 run.  At the C2 shape, K = 8,
@@ -149,8 +152,11 @@ def test_float32_input_against_reference():
             assert d["pac_area"] == pf["pac_area"][j], K
     print(f"float32 input: {same}/{total} (K, h) label vectors identical; (K, |dPAC|, max |dC|):",
           report)
-    assert max(r[1] for r in report) <= F32_MAX_DPAC, report
-    assert max(r[2] for r in report) <= F32_MAX_DC, report
+    ref_dpac = float(np.abs(pf["pac_area_nudge"] - pf["pac_area"][None, :]).max())
+    ref_dc = float(pf["max_dc_nudge"].max())
+    print(f"reference against itself under 2^-22 input nudges: max |dPAC| {ref_dpac:.6f}, max |dC| {ref_dc:.4f}")
+    assert max(r[1] for r in report) <= F32_SPREAD_FACTOR * ref_dpac, report
+    assert max(r[2] for r in report) <= ref_dc, report
     assert cc.best_k_ == meta["best_k"]
 
 
