@@ -28,7 +28,7 @@ L = engine.new_label_matrix(len(cfg["Ks"]), n, engine.pad_h(H), dev)
 inert = torch.zeros((len(cfg["Ks"]), H), dtype=torch.float32, device=dev)
 nit = torch.zeros((len(cfg["Ks"]), H), dtype=torch.int32, device=dev)
 bk = BatchedKMeans(cfg["Ks"], n_init=3, random_state=SEED, max_iter=int(os.environ.get("KM_MAXITER", 300)),
-                   workspace_budget=int(os.environ.get("KM_BUDGET_GB", 8)) << 30)
+                   workspace_budget=(int(os.environ["KM_BUDGET_GB"]) << 30) if "KM_BUDGET_GB" in os.environ else None)
 ts = []
 for r in range(reps + 1):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
